@@ -1,0 +1,210 @@
+"""Decentralized edge-split ADMM loop on MI355X (the reference's block_6 hot path).
+
+``run_admm`` implements /root/reference/block_6_admm_loop_ver2.py:15-326 with
+the node solves and edge updates on the GPU:
+
+  for k in range(max_iters):                         (:69)
+      x-update of every local node   -> NodeBatch.node_update   (:81-187)
+      halo exchange of x_j           -> HaloExchange.run (RCCL)
+      z/y update + residual partials -> NodeBatch.consensus     (:210-253)
+      statistics -> history, stop test                          (:189-206,255-289)
+
+Histories carry the reference's keys (:310-326).  One process per GPU: when
+``torch.distributed`` is initialised with world size > 1 the graph nodes are
+sharded (plan.py) and every rank returns the same ``(x_list, history)``.
+"""
+from __future__ import annotations
+
+import math
+import os
+from datetime import datetime
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .exchange import HaloExchange, assemble_stats, gather_images
+from .geometry import RayTransform
+from .plan import make_plan
+from .solver import NodeBatch
+
+HISTORY_KEYS = (
+    "primal", "dual", "pri_per_node", "dual_per_node", "obj_per_node", "obj_total",
+    "mse_sino_per_node", "mse_sino_total", "img_mse_per_node", "img_mse_total",
+    "g_norm_history", "eps_used_history", "eps_target_history",
+)
+
+DEFAULT_MU_FACTOR = 10.0  # split-Bregman penalty mu = 10 * lam_tv
+
+
+def eps_target(k: int) -> float:
+    """block_6_admm_loop_ver2.py:101-103."""
+    return 2.0 / ((k + 1) ** 1.005)
+
+
+def _common_geometry(A_list):
+    geoms = set()
+    for A in A_list:
+        if not isinstance(A, RayTransform):
+            raise TypeError(
+                "A_dense_list entries must be admm_hip RayTransform operators (matrix-free "
+                f"projector); got {type(A).__name__}.  Dense matrices are not accepted on the "
+                "GPU path -- build operators with block_2_load_odl_data.load_odl_data or "
+                "admm_hip.solver.make_operators.")
+        if A._adjoint:
+            raise ValueError("A_dense_list entry is an adjoint view")
+        geoms.add((A.geom, A.dtype, A.device))
+    if len(geoms) != 1:
+        raise NotImplementedError(
+            "all nodes must share one geometry (same angle count): the batched kernels project "
+            "every node with one angle table; choose angles_total divisible by num_nodes")
+    return geoms.pop()
+
+
+def _dist_info(group):
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
+
+
+def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
+             max_iters=10, eps_pri=1e-1, eps_dual=1e-1, verbose=True, snapshot_dir=None,
+             snapshot_every=None, snapshot_div=10, phantom_true=None, mu=None, tv_iters=10,
+             cg_iters=5, tv_kind="iso", group=None, return_tensors=False, timing=None,
+             write_params=True):
+    V_total = len(A_dense_list)
+    geom, dtype, device = _common_geometry(A_dense_list)
+    if geom.N != N:
+        raise ValueError(f"N={N} does not match the operators' N={geom.N}")
+    if sorted(G.nodes()) != list(range(V_total)):
+        raise ValueError("graph nodes must be 0..num_nodes-1")
+    mu = DEFAULT_MU_FACTOR * lam_tv if mu is None else float(mu)
+    if not mu > 0:
+        raise ValueError("mu must be > 0 (set lam_tv > 0 or pass mu explicitly)")
+    world, rank = _dist_info(group)
+    torch.cuda.set_device(device)
+    plan = make_plan(G, V_total, world, rank)
+    if snapshot_dir is not None:
+        os.makedirs(snapshot_dir, exist_ok=True)
+    if snapshot_every is None:
+        snapshot_every = max(1, max_iters // snapshot_div)  # _ver2:31-32
+    nb = NodeBatch(geom, dtype, plan, sinograms, Qij_diag_fn, rho, lam_tv, mu, tv_iters, cg_iters,
+                   tv_kind, phantom_true, device)
+    halo = HaloExchange(plan, nb.x_ext, group)
+    if world > 1:
+        dist.barrier(group=group)
+    hist = {k: [] for k in HISTORY_KEYS}
+    edges = plan.edges
+    have_ph = phantom_true is not None
+    if verbose and rank == 0:
+        print(f"Max ADMM Iteration in Block-6 B4 Loop = {max_iters}")
+    torch.cuda.synchronize()
+    t_loop = None
+    if timing is not None:
+        import time
+        t_loop = time.perf_counter()
+    iters_done = 0
+    for k in range(max_iters):
+        nb.node_update()
+        halo.run()
+        nb.consensus()
+        ns, es = assemble_stats(plan, nb.node_stats, nb.edge_stats[: len(plan.stored_edges)], group)
+        ns = ns.numpy()
+        es = es.numpy()
+        iters_done = k + 1
+        # --- node diagnostics (_ver2:145-206) ---
+        et = eps_target(k)
+        mse = ns[:, 0].copy()
+        g_norm = np.sqrt(ns[:, 1])
+        obj = 0.5 * ns[:, 0] + lam_tv * ns[:, 2] + ns[:, 3]
+        hist["g_norm_history"].append(g_norm)
+        hist["eps_used_history"].append(np.full(V_total, min(1e-2, et)))
+        hist["eps_target_history"].append(np.full(V_total, et))
+        hist["mse_sino_per_node"].append(mse)
+        hist["mse_sino_total"].append(float(np.sum(mse)))
+        img = ns[:, 4].copy() if have_ph else np.full(V_total, np.nan)
+        hist["img_mse_per_node"].append(img)
+        hist["img_mse_total"].append(float(np.sum(img)))
+        # --- residuals in G.edges() order (_ver2:232-258) ---
+        r2 = 0.0
+        s2 = 0.0
+        pri = np.zeros(V_total)
+        dua = np.zeros(V_total)
+        for ge, (a, b) in enumerate(edges):
+            ra2, rb2, dz2 = float(es[ge, 0]), float(es[ge, 1]), float(es[ge, 2])
+            r2 += ra2 + rb2
+            pri[a] += ra2
+            pri[b] += rb2
+            s2 += rho * rho * dz2
+            dua[a] += rho * rho * dz2
+            dua[b] += rho * rho * dz2
+        pn, dn = math.sqrt(r2), math.sqrt(s2)
+        hist["primal"].append(pn)
+        hist["dual"].append(dn)
+        hist["obj_per_node"].append(obj)
+        hist["obj_total"].append(float(np.sum(obj)))
+        hist["pri_per_node"].append(np.sqrt(pri))
+        hist["dual_per_node"].append(np.sqrt(dua))
+        if snapshot_dir is not None and ((k + 1) % snapshot_every == 0):
+            _snapshot(snapshot_dir, k, plan, nb.x_local, N)
+        if verbose and rank == 0 and k % 10 == 0:
+            print(f"iter {k}, primal {pn:.3e}, dual {dn:.3e}")
+        if pn < eps_pri and dn < eps_dual:
+            if verbose and rank == 0:
+                print(f"stopped at iter {k}, primal {pn:.3e}, dual {dn:.3e}")
+            break
+    torch.cuda.synchronize()
+    if timing is not None:
+        import time
+        timing["loop_s"] = time.perf_counter() - t_loop
+        timing["iters"] = iters_done
+        timing["V_total"] = V_total
+    if write_params and rank == 0:
+        _write_params(snapshot_dir, rho, lam_tv, V_total, mu, tv_iters, cg_iters)
+    X = gather_images(plan, nb.x_local, group)
+    if return_tensors:
+        return [X[i] for i in range(V_total)], hist
+    Xh = X.to("cpu").numpy()
+    return [Xh[i].copy() for i in range(V_total)], hist
+
+
+def _snapshot(snapshot_dir, k, plan, x_local, N):
+    """_ver2:269-281: iter_XXXX_node_i.npy (C-order reshape) + .png."""
+    it_tag = f"iter_{k + 1:04d}"
+    xs = x_local.to("cpu").numpy()
+    try:
+        import matplotlib
+        matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+    except Exception:  # pragma: no cover
+        plt = None
+    for r, g in enumerate(plan.local_nodes):
+        img = xs[r].reshape(N, N)
+        np.save(os.path.join(snapshot_dir, f"{it_tag}_node_{g}.npy"), img)
+        if plt is not None:
+            plt.figure(figsize=(5, 5))
+            plt.imshow(img, cmap="gray")
+            plt.title(f"{it_tag}  node {g}")
+            plt.axis("off")
+            plt.tight_layout()
+            plt.savefig(os.path.join(snapshot_dir, f"{it_tag}_node_{g}.png"), dpi=220)
+            plt.close()
+
+
+def _write_params(snapshot_dir, rho, lam_tv, V, mu, tv_iters, cg_iters):
+    """_ver2:291-306 admm_internal_params.txt."""
+    try:
+        log_dir = snapshot_dir if snapshot_dir is not None else os.getcwd()
+        os.makedirs(log_dir, exist_ok=True)
+        with open(os.path.join(log_dir, "admm_internal_params.txt"), "w") as f:
+            f.write("===== ADMM Internal Parameters =====\n")
+            f.write(f"rho = {rho}\n")
+            f.write(f"lambda_tv = {lam_tv}\n")
+            f.write(f"Number of nodes = {V}\n")
+            f.write("Calib alpha = 1.0\n")
+            f.write("Eps cap = 0.01\n")
+            f.write(f"Split-Bregman mu = {mu}\n")
+            f.write(f"Inner iterations (tv x cg) = {tv_iters} x {cg_iters}\n")
+            f.write(f"Date-Time: {datetime.now().strftime('%Y-%m-%d %H:%M:%S')}\n")
+    except Exception as e:  # pragma: no cover
+        print(f"[WARN] Could not save internal params: {e}")

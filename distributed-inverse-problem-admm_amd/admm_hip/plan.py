@@ -1,0 +1,128 @@
+"""Graph-node sharding plan: which nodes, edges and halo images live on a rank.
+
+Pure host logic (no GPU), exercised by the world-size-2 gloo tests.
+
+* Nodes are split into contiguous blocks, one per rank.
+* Edges are the reference's ``G.edges()`` in order, canonicalised to
+  (min, max) (block_6_admm_loop_ver2.py:39-43,211-212).  A rank stores every
+  edge incident to one of its nodes; an edge whose endpoints live on two ranks
+  is stored (and updated, bitwise identically) on both.  Its statistics are
+  reported by the owner of the lower endpoint.
+* The only data a rank needs from others is x_j of its halo nodes (remote
+  neighbours): with the single-y edge form z and y are computed redundantly
+  at both ends, so no second exchange is needed.
+* Incident edge-ends of a node are listed in ``G.neighbors(i)`` order so the
+  neighbour sums c_i = sum_j q_ij v_ij add in the reference's order
+  (block_6_admm_loop_ver2.py:87).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+
+def node_ranges(V: int, world: int) -> list[tuple[int, int]]:
+    """Contiguous near-equal blocks [lo, hi) of graph nodes per rank."""
+    bounds = np.linspace(0, V, world + 1)
+    cuts = [int(round(b)) for b in bounds]
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def owner_of(ranges: list[tuple[int, int]], node: int) -> int:
+    for r, (lo, hi) in enumerate(ranges):
+        if lo <= node < hi:
+            return r
+    raise KeyError(node)
+
+
+@dataclass
+class ShardPlan:
+    V_total: int
+    world: int
+    rank: int
+    edges: list  # global canonical edges (a, b), a < b, in G.edges() order
+    ranges: list
+    local_nodes: list = field(default_factory=list)
+    halo_nodes: list = field(default_factory=list)
+    xrow: dict = field(default_factory=dict)        # global node -> x_ext row
+    stored_edges: list = field(default_factory=list)  # global edge ids stored here
+    edge_a_row: list = field(default_factory=list)
+    edge_b_row: list = field(default_factory=list)
+    owned_edge: list = field(default_factory=list)  # bool per stored edge
+    inc_off: list = field(default_factory=list)
+    inc_edge: list = field(default_factory=list)    # stored-edge slot
+    inc_nbr: list = field(default_factory=list)     # neighbour global id (for Qij_diag_fn)
+    inc_sign: list = field(default_factory=list)
+    send: dict = field(default_factory=dict)        # peer -> sorted local nodes it needs
+    recv: dict = field(default_factory=dict)        # peer -> sorted halo nodes it sends
+
+    @property
+    def V(self) -> int:
+        return len(self.local_nodes)
+
+    @property
+    def n_xext(self) -> int:
+        return len(self.local_nodes) + len(self.halo_nodes)
+
+    def use_allgather(self) -> bool:
+        """All-gather when a rank needs most remote images (dense / ER graphs)."""
+        if self.world == 1:
+            return False
+        remote = self.V_total - self.V
+        return remote > 0 and len(self.halo_nodes) * 2 > remote
+
+
+def make_plan(G, V_total: int, world: int = 1, rank: int = 0) -> ShardPlan:
+    edges = [(min(i, j), max(i, j)) for i, j in G.edges()]
+    if len(set(edges)) != len(edges):
+        raise ValueError("graph has duplicate edges")
+    for a, b in edges:
+        if a == b:
+            raise ValueError("self loops are not supported")
+        if not (0 <= a < V_total and 0 <= b < V_total):
+            raise ValueError("edge endpoint out of range")
+    ranges = node_ranges(V_total, world)
+    lo, hi = ranges[rank]
+    P = ShardPlan(V_total=V_total, world=world, rank=rank, edges=edges, ranges=ranges)
+    P.local_nodes = list(range(lo, hi))
+    local = set(P.local_nodes)
+    halo = set()
+    for a, b in edges:
+        if a in local and b not in local:
+            halo.add(b)
+        if b in local and a not in local:
+            halo.add(a)
+    P.halo_nodes = sorted(halo)
+    for r, g in enumerate(P.local_nodes + P.halo_nodes):
+        P.xrow[g] = r
+    eidx = {}
+    for ge, (a, b) in enumerate(edges):
+        if a in local or b in local:
+            eidx[ge] = len(P.stored_edges)
+            P.stored_edges.append(ge)
+            P.edge_a_row.append(P.xrow[a])
+            P.edge_b_row.append(P.xrow[b])
+            P.owned_edge.append(owner_of(ranges, a) == rank)
+    edge_of = {e: ge for ge, e in enumerate(edges)}
+    P.inc_off = [0]
+    for g in P.local_nodes:
+        for j in G.neighbors(g):
+            e = (min(g, j), max(g, j))
+            P.inc_edge.append(eidx[edge_of[e]])
+            P.inc_nbr.append(int(j))
+            P.inc_sign.append(1 if g == e[0] else -1)
+        P.inc_off.append(len(P.inc_edge))
+    for peer in range(world):
+        if peer == rank:
+            continue
+        plo, phi = ranges[peer]
+        P.recv[peer] = [g for g in P.halo_nodes if plo <= g < phi]
+        need = set()
+        for a, b in edges:
+            if a in local and plo <= b < phi:
+                need.add(a)
+            if b in local and plo <= a < phi:
+                need.add(b)
+        P.send[peer] = sorted(need)
+    return P

@@ -1,0 +1,156 @@
+"""Device-resident node batch: the per-GPU state of the decentralized ADMM hot path.
+
+Holds, in HBM, everything one GPU needs for its graph nodes (layout: DESIGN.md
+"Data layout in HBM") and drives the C-ABI entry points:
+
+* ``node_update()``  -- x-update of every local node (admm_node_update; replaces
+  block_6_admm_loop_ver2.py:81-197: neighbour gather, CVXPY/SCS solve, g check);
+* ``consensus()``    -- z / y / residual partials of every stored edge
+  (admm_consensus; replaces block_6_admm_loop_ver2.py:210-253).
+
+Both are stream-ordered on the current torch stream and replay hipGraphs
+recorded at bind time.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import hashlib
+
+import numpy as np
+import torch
+
+from . import _lib
+from .geometry import ParallelBeamGeometry, RayTransform, current_stream_handle, _Ctx
+from .plan import ShardPlan
+
+
+def _as_f64_tensor(v, n: int, dev) -> torch.Tensor:
+    t = torch.as_tensor(v) if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))
+    t = t.reshape(-1)
+    if t.numel() != n:
+        raise ValueError(f"vector has {t.numel()} entries, expected {n}")
+    return t.to(device=dev, dtype=torch.float64)
+
+
+def _vec_key(t: torch.Tensor):
+    h = hashlib.blake2b(t.detach().to("cpu").numpy().tobytes(), digest_size=16).hexdigest()
+    return ("hash", h)
+
+
+class NodeBatch:
+    def __init__(self, geom: ParallelBeamGeometry, dtype: str, plan: ShardPlan, sinograms,
+                 Qij_diag_fn, rho: float, lam: float, mu: float, tv_iters: int = 10,
+                 cg_iters: int = 5, tv_kind: str = "iso", phantom=None, device: int = 0):
+        self.lib = _lib.load()
+        self.geom = geom
+        self.plan = plan
+        self.dtype = dtype
+        self.device = device
+        dev = torch.device("cuda", device)
+        self.dev = dev
+        n, m = geom.n, geom.m
+        V = plan.V
+        if V < 1:
+            raise ValueError("rank owns no graph nodes")
+        sdt = torch.float64 if dtype == "float64" else torch.float32
+        self.ctx = _Ctx(geom, dtype, device, max_images=max(1, V))
+        self.x_ext = torch.zeros((plan.n_xext, n), dtype=torch.float64, device=dev)
+        self.d = torch.zeros((V, 2, n), dtype=torch.float64, device=dev)
+        self.e = torch.zeros((V, 2, n), dtype=torch.float64, device=dev)
+        self.atb = torch.zeros((V, n), dtype=torch.float64, device=dev)
+        self.b = torch.empty((V, m), dtype=sdt, device=dev)
+        for k, g in enumerate(plan.local_nodes):
+            s = sinograms[g]
+            st = s if isinstance(s, torch.Tensor) else torch.as_tensor(np.asarray(s))
+            st = st.reshape(-1)
+            if st.numel() != m:
+                raise ValueError(f"sinogram of node {g} has {st.numel()} entries, expected {m}")
+            self.b[k].copy_(st.to(device=dev, dtype=sdt))
+        self.phantom = None
+        if phantom is not None:
+            self.phantom = _as_f64_tensor(phantom, n, dev)
+        # precision vectors q_ij, deduplicated into slots
+        E = len(plan.stored_edges)
+        keyfn = getattr(Qij_diag_fn, "qslot_key", None)
+        slots, qvecs, inc_qslot = {}, [], []
+        for k, g in enumerate(plan.local_nodes):
+            for q in range(plan.inc_off[k], plan.inc_off[k + 1]):
+                j = plan.inc_nbr[q]
+                key = keyfn(g, j) if keyfn is not None else None
+                if key is not None and key in slots:
+                    inc_qslot.append(slots[key])
+                    continue
+                vec = _as_f64_tensor(Qij_diag_fn(g, j), n, dev)
+                if key is None:
+                    key = _vec_key(vec)
+                if key not in slots:
+                    slots[key] = len(qvecs)
+                    qvecs.append(vec)
+                inc_qslot.append(slots[key])
+        self.q = torch.stack(qvecs) if qvecs else torch.zeros((1, n), dtype=torch.float64, device=dev)
+        self.n_qslots = len(qvecs)
+        ii = lambda a: torch.tensor(a if len(a) else [0], dtype=torch.int32, device=dev)  # noqa: E731
+        self.inc_off = ii(plan.inc_off)
+        self.inc_edge = ii(plan.inc_edge)
+        self.inc_sign = ii(plan.inc_sign)
+        self.inc_qslot = ii(inc_qslot)
+        self.edge_a = ii(plan.edge_a_row)
+        self.edge_b = ii(plan.edge_b_row)
+        self.y = torch.zeros((max(E, 1), n), dtype=torch.float64, device=dev)
+        self.z = torch.zeros((max(E, 1), n), dtype=torch.float64, device=dev)
+        # D_i = sum_j q_ij  (constant across iterations; setup)
+        self.dsum = torch.zeros((V, n), dtype=torch.float64, device=dev)
+        for k in range(V):
+            for q in range(plan.inc_off[k], plan.inc_off[k + 1]):
+                self.dsum[k] += self.q[inc_qslot[q]]
+        self.node_stats = torch.zeros((V, _lib.NODE_STATS), dtype=torch.float64, device=dev)
+        self.edge_stats = torch.zeros((max(E, 1), _lib.EDGE_STATS), dtype=torch.float64, device=dev)
+        self.params = dict(rho=float(rho), lam=float(lam), mu=float(mu), tv_iters=int(tv_iters),
+                           cg_iters=int(cg_iters), tv_kind=tv_kind)
+        p = lambda t: C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)  # noqa: E731
+        self.cb = _lib.Batch(
+            V, plan.n_xext, E, int(tv_iters), int(cg_iters),
+            _lib.ADMM_TV_ANISO if tv_kind == "aniso" else _lib.ADMM_TV_ISO,
+            float(rho), float(lam), float(mu),
+            p(self.x_ext), p(self.d), p(self.e), p(self.atb), p(self.dsum), p(self.b), p(self.phantom),
+            p(self.y), p(self.z), p(self.q), p(self.edge_a), p(self.edge_b), p(self.inc_off),
+            p(self.inc_edge), p(self.inc_qslot), p(self.inc_sign), p(self.node_stats),
+            p(self.edge_stats))
+        torch.cuda.synchronize(dev)
+        _lib.check(self.lib.admm_batch_bind(self.ctx.h, C.byref(self.cb)), "admm_batch_bind")
+        _lib.check(self.lib.admm_batch_atb(self.ctx.h, p(self.atb), C.c_void_p(self._s())),
+                   "admm_batch_atb")
+
+    def _s(self) -> int:
+        return current_stream_handle(self.dev)
+
+    @property
+    def V(self) -> int:
+        return self.plan.V
+
+    @property
+    def x_local(self) -> torch.Tensor:
+        return self.x_ext[: self.plan.V]
+
+    def node_update(self) -> None:
+        _lib.check(self.lib.admm_node_update(self.ctx.h, C.c_void_p(self._s())), "admm_node_update")
+
+    def consensus(self) -> None:
+        if self.plan.stored_edges:
+            _lib.check(self.lib.admm_consensus(self.ctx.h, C.c_void_p(self._s())), "admm_consensus")
+
+    def time_forward(self, reps: int = 20) -> float:
+        ms = C.c_double()
+        _lib.check(self.lib.admm_time_forward(self.ctx.h, reps, C.c_void_p(self._s()), C.byref(ms)),
+                   "admm_time_forward")
+        return ms.value
+
+
+def make_operators(N: int, num_nodes: int, angles_total: int | None = None, dtype: str = "float32",
+                   device: int = 0, det_width_factor: float = 1.0) -> list[RayTransform]:
+    """Per-node ray transforms of block_2_load_odl_data.py:34-83 (all nodes span [0, pi))."""
+    from .geometry import split_angles
+    if angles_total is None:
+        angles_total = max(180, 3 * N)
+    per = split_angles(angles_total, num_nodes)
+    return [RayTransform(ParallelBeamGeometry(N, a, det_width_factor), dtype, device) for a in per]

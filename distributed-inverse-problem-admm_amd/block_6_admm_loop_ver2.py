@@ -1,0 +1,34 @@
+"""Drop-in for /root/reference/block_6_admm_loop_ver2.py (the canonical ADMM loop).
+
+Same signature (:15-20) and history keys (:310-326); the node solves and edge
+updates run on MI355X (admm_hip.admm.run_admm).  Extra keyword arguments:
+
+* ``mu``        split-Bregman penalty (default 10 * lam_tv)
+* ``tv_iters``  split-Bregman rounds per x-update (default 10)
+* ``cg_iters``  CG steps per round (default 5)
+* ``tv_kind``   "iso" (default) or "aniso"
+* ``group``     torch.distributed process group (default: WORLD if initialised)
+
+``max_inner_iters`` is accepted and, as in the reference, unused.
+"""
+from __future__ import annotations
+
+from admm_hip.admm import run_admm
+
+
+def decentralized_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn,
+                       N, lam_tv=0.01, rho=1.0,
+                       max_iters=10, max_inner_iters=100,
+                       eps_pri=1e-1, eps_dual=1e-1,
+                       verbose=True, snapshot_dir=None,
+                       snapshot_every=None, snapshot_div=10, phantom_true=None,
+                       mu=None, tv_iters=10, cg_iters=5, tv_kind="iso", group=None,
+                       write_params=True):
+    """Returns (x_list, history) like block_6_admm_loop_ver2.py:310-326."""
+    del max_inner_iters  # accepted but unused, as in the reference (_ver2:17)
+    return run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=lam_tv, rho=rho,
+                    max_iters=max_iters, eps_pri=eps_pri, eps_dual=eps_dual, verbose=verbose,
+                    snapshot_dir=snapshot_dir, snapshot_every=snapshot_every,
+                    snapshot_div=snapshot_div, phantom_true=phantom_true, mu=mu,
+                    tv_iters=tv_iters, cg_iters=cg_iters, tv_kind=tv_kind, group=group,
+                    write_params=write_params)

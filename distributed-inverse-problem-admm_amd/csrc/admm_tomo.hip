@@ -1,0 +1,600 @@
+// admm_tomo.hip -- C-ABI implementation (include/admm_tomo.h) for MI355X (gfx950).
+//
+// Host side of the hot path: geometry tables, scratch, and the x-update /
+// consensus sequences.  A bound batch's sequences are recorded once as
+// hipGraphs and replayed every ADMM iteration (launch-bound at small N
+// otherwise: ~170 kernels per x-update).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/admm_tomo.h"
+#include "kernels.hpp"
+
+using namespace admm;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                          \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess)                                                                     \
+      return fail(ADMM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e) + " @" +     \
+                                  std::to_string(__LINE__));                                  \
+  } while (0)
+
+#define CHECK_LAUNCH() HIPCHK(hipGetLastError())
+
+size_t dsize(int dtype) { return dtype == ADMM_DTYPE_F64 ? 8 : 4; }
+
+struct Buf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+int ensure(Buf& b, size_t bytes) {
+  if (b.bytes >= bytes && b.p) return ADMM_OK;
+  if (b.p) HIPCHK(hipFree(b.p));
+  b.p = nullptr;
+  b.bytes = 0;
+  if (bytes == 0) return ADMM_OK;
+  HIPCHK(hipMalloc(&b.p, bytes));
+  HIPCHK(hipMemset(b.p, 0, bytes));
+  b.bytes = bytes;
+  return ADMM_OK;
+}
+}  // namespace
+
+struct admm_ctx {
+  admm_geom g{};
+  int dtype = ADMM_DTYPE_F32;
+  int device = 0;
+  int max_images = 0;
+  int npix = 0, mrays = 0;
+  FwdAngle* fang = nullptr;
+  BackAngle* bang = nullptr;
+  hipStream_t cap = nullptr;  // private capture stream
+
+  // operator-API scratch
+  Buf op_img, op_imgT;
+
+  // batch
+  bool bound = false;
+  admm_batch b{};
+  Buf xs, xsT, p, pT, Hp, sino, r, c, d2, e2;
+  Buf partH, partRR, partS, partD, partE;
+  Buf redH, rrslot;
+  int P_back = 0, P_tile = 0, P_fwd = 0, P_edge = 0;
+  hipGraph_t g_update = nullptr, g_cons = nullptr;
+  hipGraphExec_t x_update = nullptr, x_cons = nullptr;
+  bool use_graph = true;
+};
+
+namespace {
+
+int vb_for(int V) { return V >= 5 ? 8 : (V >= 3 ? 4 : (V == 2 ? 2 : 1)); }
+
+template <typename T, int VB, int MODE>
+void launch_fwd_vb(admm_ctx* C, const T* img, const T* imgT, T* sino, const T* b, double* part, int V,
+                   hipStream_t s) {
+  dim3 grid((C->g.n_det + kFwdRays - 1) / kFwdRays, C->g.n_angles, (V + VB - 1) / VB);
+  hipLaunchKernelGGL((k_fwd<T, VB, MODE>), grid, dim3(kBlock), 0, s, img, imgT, sino, b, part, C->fang,
+                     C->g.N, C->g.n_det, C->g.n_angles, V);
+}
+
+template <typename T, int MODE>
+int launch_fwd(admm_ctx* C, const T* img, const T* imgT, T* sino, const T* b, double* part, int V,
+               hipStream_t s) {
+  switch (vb_for(V)) {
+    case 8: launch_fwd_vb<T, 8, MODE>(C, img, imgT, sino, b, part, V, s); break;
+    case 4: launch_fwd_vb<T, 4, MODE>(C, img, imgT, sino, b, part, V, s); break;
+    case 2: launch_fwd_vb<T, 2, MODE>(C, img, imgT, sino, b, part, V, s); break;
+    default: launch_fwd_vb<T, 1, MODE>(C, img, imgT, sino, b, part, V, s); break;
+  }
+  CHECK_LAUNCH();
+  return ADMM_OK;
+}
+
+template <typename T, int VB, int MODE>
+void launch_back_vb(admm_ctx* C, const BackArgs<T>& a, int V, hipStream_t s) {
+  const int N = C->g.N;
+  dim3 grid((N + kBackTileJ - 1) / kBackTileJ, (N + kBackTileI - 1) / kBackTileI,
+            MODE == BACK_WSQ ? 1 : (V + VB - 1) / VB);
+  hipLaunchKernelGGL((k_back<T, VB, MODE>), grid, dim3(kBlock), 0, s, a);
+}
+
+template <typename T, int MODE>
+int launch_back(admm_ctx* C, BackArgs<T> a, int V, hipStream_t s) {
+  a.ang = C->bang;
+  a.N = C->g.N;
+  a.n_det = C->g.n_det;
+  a.n_ang = C->g.n_angles;
+  a.V = V;
+  if (MODE == BACK_WSQ) {
+    launch_back_vb<T, 1, MODE>(C, a, 1, s);
+  } else {
+    switch (vb_for(V)) {
+      case 8: launch_back_vb<T, 8, MODE>(C, a, V, s); break;
+      case 4: launch_back_vb<T, 4, MODE>(C, a, V, s); break;
+      case 2: launch_back_vb<T, 2, MODE>(C, a, V, s); break;
+      default: launch_back_vb<T, 1, MODE>(C, a, V, s); break;
+    }
+  }
+  CHECK_LAUNCH();
+  return ADMM_OK;
+}
+
+int back_partitions(admm_ctx* C) {
+  const int N = C->g.N;
+  return ((N + kBackTileJ - 1) / kBackTileJ) * ((N + kBackTileI - 1) / kBackTileI);
+}
+dim3 tile_grid(admm_ctx* C, int V) {
+  const int N = C->g.N;
+  return dim3((N + kTile - 1) / kTile, (N + kTile - 1) / kTile, V);
+}
+
+int launch_reduce(const double* part, int rows, int P, double* out, int G, int ostride, int ooff, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce_rows, dim3(rows), dim3(kBlock), 0, s, part, P, out, G, ostride, ooff);
+  CHECK_LAUNCH();
+  return ADMM_OK;
+}
+
+#define RET(expr)                 \
+  do {                            \
+    int _rc = (expr);             \
+    if (_rc != ADMM_OK) return _rc; \
+  } while (0)
+
+// --------------------------------------------------------------------------
+// the x-update sequence for the bound batch (replaces block_6_admm_loop_ver2.py:81-197)
+// --------------------------------------------------------------------------
+template <typename T>
+int enqueue_update(admm_ctx* C, hipStream_t s) {
+  const admm_batch& B = C->b;
+  const int V = B.V, N = C->g.N;
+  const size_t npix = (size_t)N * N;
+  T* xs = (T*)C->xs.p;
+  T* xsT = (T*)C->xsT.p;
+  T* p = (T*)C->p.p;
+  T* pT = (T*)C->pT.p;
+  T* Hp = (T*)C->Hp.p;
+  T* sino = (T*)C->sino.p;
+  double* r = (double*)C->r.p;
+  double* c = (double*)C->c.p;
+  double* redH = (double*)C->redH.p;
+  double* rrslot = (double*)C->rrslot.p;
+  const dim3 tg = tile_grid(C, V);
+  const int Pt = C->P_tile, Pb = C->P_back;
+
+  // 1. neighbour gather: c = sum_j q_ij (z_ij - y_ij,i); xs = (T) x
+  hipLaunchKernelGGL(k_gather<T>, tg, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.q, B.inc_off, B.inc_edge,
+                     B.inc_qslot, B.inc_sign, c, xs, xsT, N);
+  CHECK_LAUNCH();
+  // 2-4. r = A^T b + rho c + mu K^T(d - e) - H x,  p = r,  rr
+  RET((launch_fwd<T, 0>(C, xs, xsT, sino, nullptr, nullptr, V, s)));
+  {
+    BackArgs<T> a{};
+    a.sino = sino;
+    a.out_t = p;
+    a.out_d = r;
+    a.part = (double*)C->partRR.p;
+    a.pin = xs;
+    a.dsum = B.dsum;
+    a.atb = B.atb;
+    a.cvec = c;
+    a.dvar = B.d;
+    a.evar = B.e;
+    a.rho = B.rho;
+    a.lam = B.lam;
+    a.mu = B.mu;
+    RET((launch_back<T, BACK_INIT>(C, a, V, s)));
+  }
+  RET(launch_reduce((double*)C->partRR.p, V, Pb, rrslot, 1, 1, 0, s));
+  hipLaunchKernelGGL(k_transpose<T>, tg, dim3(kBlock), 0, s, p, pT, N);
+  CHECK_LAUNCH();
+
+  const double tau = B.lam / B.mu;
+  double* dcur = B.d;
+  double* ecur = B.e;
+  double* dnxt = (double*)C->d2.p;
+  double* enxt = (double*)C->e2.p;
+  const int K = B.cg_iters, Tt = B.tv_iters;
+  for (int t = 0; t < Tt; ++t) {
+    for (int kk = 0; kk < K; ++kk) {
+      const int it = t * K + kk;
+      RET((launch_fwd<T, 0>(C, p, pT, sino, nullptr, nullptr, V, s)));
+      BackArgs<T> a{};
+      a.sino = sino;
+      a.out_t = Hp;
+      a.part = (double*)C->partH.p;
+      a.pin = p;
+      a.r = r;
+      a.dsum = B.dsum;
+      a.rho = B.rho;
+      a.lam = B.lam;
+      a.mu = B.mu;
+      RET((launch_back<T, BACK_H>(C, a, V, s)));
+      RET(launch_reduce((double*)C->partH.p, 3 * V, Pb, redH, 1, 1, 0, s));
+      hipLaunchKernelGGL(k_cg_update<T>, tg, dim3(kBlock), 0, s, B.x_ext, r, p, pT, Hp, redH,
+                         rrslot + (size_t)it * V, rrslot + (size_t)(it + 1) * V, N);
+      CHECK_LAUNCH();
+    }
+    const bool last = (t + 1 == Tt);
+    if (!last) {
+      hipLaunchKernelGGL((k_tv_update<T, false>), tg, dim3(kBlock), 0, s, B.x_ext, dcur, ecur, dnxt, enxt, r, p,
+                         pT, (double*)C->partRR.p, tau, B.mu, B.tv_kind, N);
+      CHECK_LAUNCH();
+      RET(launch_reduce((double*)C->partRR.p, V, Pt, rrslot + (size_t)(t + 1) * K * V, 1, 1, 0, s));
+    } else {
+      hipLaunchKernelGGL((k_tv_update<T, true>), tg, dim3(kBlock), 0, s, B.x_ext, dcur, ecur, dnxt, enxt, r, xs,
+                         xsT, (double*)nullptr, tau, B.mu, B.tv_kind, N);
+      CHECK_LAUNCH();
+    }
+    std::swap(dcur, dnxt);
+    std::swap(ecur, enxt);
+  }
+  if (dcur != B.d) {  // odd number of rounds: state ended in scratch
+    HIPCHK(hipMemcpyAsync(B.d, dcur, 2 * V * npix * sizeof(double), hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(B.e, ecur, 2 * V * npix * sizeof(double), hipMemcpyDeviceToDevice, s));
+  }
+  // diagnostics epilogue: s = A x - b, ||s||^2, g, TV, quad, image error
+  RET((launch_fwd<T, 1>(C, xs, xsT, sino, (const T*)B.b, (double*)C->partS.p, V, s)));
+  {
+    BackArgs<T> a{};
+    a.sino = sino;
+    a.part = (double*)C->partD.p;
+    a.dsum = B.dsum;
+    a.cvec = c;
+    a.x = B.x_ext;
+    a.phantom = B.phantom;
+    a.yv = B.y;
+    a.zv = B.z;
+    a.qv = B.q;
+    a.inc_off = B.inc_off;
+    a.inc_edge = B.inc_edge;
+    a.inc_qslot = B.inc_qslot;
+    a.inc_sign = B.inc_sign;
+    a.rho = B.rho;
+    a.lam = B.lam;
+    a.mu = B.mu;
+    a.tv_kind = B.tv_kind;
+    RET((launch_back<T, BACK_DIAG>(C, a, V, s)));
+  }
+  RET(launch_reduce((double*)C->partS.p, V, C->P_fwd, B.node_stats, 1, ADMM_NODE_STATS, ADMM_NODE_STAT_MSE_SINO, s));
+  RET(launch_reduce((double*)C->partD.p, 4 * V, Pb, B.node_stats, 4, ADMM_NODE_STATS, ADMM_NODE_STAT_G2, s));
+  return ADMM_OK;
+}
+
+int enqueue_consensus(admm_ctx* C, hipStream_t s) {
+  const admm_batch& B = C->b;
+  if (B.n_edges == 0) return ADMM_OK;
+  const int npix = C->npix;
+  dim3 grid((npix + kBlock * 4 - 1) / (kBlock * 4), B.n_edges);
+  hipLaunchKernelGGL(k_consensus, grid, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.edge_a, B.edge_b,
+                     (double*)C->partE.p, npix);
+  CHECK_LAUNCH();
+  RET(launch_reduce((double*)C->partE.p, 3 * B.n_edges, C->P_edge, B.edge_stats, 1, 1, 0, s));
+  return ADMM_OK;
+}
+
+int free_graphs(admm_ctx* C) {
+  if (C->x_update) HIPCHK(hipGraphExecDestroy(C->x_update));
+  if (C->g_update) HIPCHK(hipGraphDestroy(C->g_update));
+  if (C->x_cons) HIPCHK(hipGraphExecDestroy(C->x_cons));
+  if (C->g_cons) HIPCHK(hipGraphDestroy(C->g_cons));
+  C->x_update = nullptr;
+  C->g_update = nullptr;
+  C->x_cons = nullptr;
+  C->g_cons = nullptr;
+  return ADMM_OK;
+}
+
+template <typename F>
+int capture(admm_ctx* C, F&& fn, hipGraph_t* g, hipGraphExec_t* x) {
+  HIPCHK(hipStreamBeginCapture(C->cap, hipStreamCaptureModeThreadLocal));
+  int rc = fn(C->cap);
+  hipGraph_t graph = nullptr;
+  hipError_t e = hipStreamEndCapture(C->cap, &graph);
+  if (rc != ADMM_OK) {
+    if (graph) (void)hipGraphDestroy(graph);
+    return rc;
+  }
+  if (e != hipSuccess) return fail(ADMM_E_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+  HIPCHK(hipGraphInstantiate(x, graph, nullptr, nullptr, 0));
+  *g = graph;
+  return ADMM_OK;
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+int admm_abi_version(void) { return ADMM_ABI_VERSION; }
+const char* admm_last_error(void) { return g_err.c_str(); }
+
+int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_images, int device) {
+  if (!out || !geom) return fail(ADMM_E_INVALID, "null argument");
+  *out = nullptr;
+  const admm_geom g = *geom;
+  if (g.N < 2 || g.n_angles < 1 || g.n_det < 1) return fail(ADMM_E_INVALID, "bad geometry sizes");
+  if (dtype != ADMM_DTYPE_F32 && dtype != ADMM_DTYPE_F64) return fail(ADMM_E_INVALID, "bad dtype");
+  if (max_images < 1) return fail(ADMM_E_INVALID, "max_images < 1");
+  const double h = 2.0 / g.N;
+  const double hd = (g.det_max - g.det_min) / g.n_det;
+  if (!(hd > 0)) return fail(ADMM_E_INVALID, "det_max <= det_min");
+  if (hd < h * (1.0 - 1e-9))
+    return fail(ADMM_E_INVALID, "detector spacing finer than the pixel size is not supported "
+                                "(det_width_factor must be >= 1 with n_det = N)");
+  const size_t npix = (size_t)g.N * g.N, m = (size_t)g.n_angles * g.n_det;
+  if ((size_t)max_images * npix * 8 >= (1ull << 31) || (size_t)max_images * m * 8 >= (1ull << 31))
+    return fail(ADMM_E_INVALID, "batch too large for 32-bit buffer offsets; split it across contexts");
+  HIPCHK(hipSetDevice(device));
+  admm_ctx* C = new admm_ctx();
+  C->g = g;
+  C->dtype = dtype;
+  C->device = device;
+  C->max_images = max_images;
+  C->npix = (int)npix;
+  C->mrays = (int)m;
+  const char* ng = getenv("ADMM_NO_GRAPH");
+  C->use_graph = !(ng && ng[0] == '1');
+
+  // geometry tables, float64 (oracle/geometry.py)
+  std::vector<FwdAngle> fa(g.n_angles);
+  std::vector<BackAngle> ba(g.n_angles);
+  const double c0 = 0.5 * (g.N - 1);
+  for (int t = 0; t < g.n_angles; ++t) {
+    const double th = g.angle_min + (t + 0.5) * (g.angle_max - g.angle_min) / g.n_angles;
+    const double cs = std::cos(th), sn = std::sin(th);
+    const bool caseA = std::fabs(cs) >= std::fabs(sn);
+    const double al = caseA ? cs : sn, be = caseA ? sn : cs;
+    fa[t].A0 = c0 + (g.det_min / h + 0.5 * hd / h + c0 * be) / al;
+    fa[t].A1 = (hd / h) / al;
+    fa[t].dl = -be / al;
+    fa[t].L = (float)(h / std::fabs(al));
+    fa[t].caseA = caseA ? 1 : 0;
+    ba[t].Bi = cs * h / hd;
+    ba[t].Bj = sn * h / hd;
+    ba[t].B0 = -c0 * (ba[t].Bi + ba[t].Bj) - g.det_min / hd - 0.5;
+    ba[t].slope = (float)((hd / h) / std::fabs(al));
+    ba[t].L = (float)(h / std::fabs(al));
+  }
+  hipError_t e1 = hipMalloc(&C->fang, fa.size() * sizeof(FwdAngle));
+  hipError_t e2 = hipMalloc(&C->bang, ba.size() * sizeof(BackAngle));
+  if (e1 != hipSuccess || e2 != hipSuccess) {
+    delete C;
+    return fail(ADMM_E_HIP, "hipMalloc geometry tables");
+  }
+  HIPCHK(hipMemcpy(C->fang, fa.data(), fa.size() * sizeof(FwdAngle), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(C->bang, ba.data(), ba.size() * sizeof(BackAngle), hipMemcpyHostToDevice));
+  HIPCHK(hipStreamCreateWithFlags(&C->cap, hipStreamNonBlocking));
+  *out = C;
+  return ADMM_OK;
+}
+
+int admm_ctx_destroy(admm_ctx* C) {
+  if (!C) return ADMM_OK;
+  (void)hipSetDevice(C->device);
+  (void)hipDeviceSynchronize();
+  free_graphs(C);
+  Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->r, &C->c,
+                 &C->d2, &C->e2, &C->partH, &C->partRR, &C->partS, &C->partD, &C->partE, &C->redH, &C->rrslot};
+  for (Buf* b : bufs)
+    if (b->p) (void)hipFree(b->p);
+  if (C->fang) (void)hipFree(C->fang);
+  if (C->bang) (void)hipFree(C->bang);
+  if (C->cap) (void)hipStreamDestroy(C->cap);
+  delete C;
+  return ADMM_OK;
+}
+
+int admm_project_fwd(admm_ctx* C, const void* img, void* sino, int nimg, void* stream) {
+  if (!C || !img || !sino) return fail(ADMM_E_INVALID, "null argument");
+  if (nimg < 1 || nimg > C->max_images) return fail(ADMM_E_INVALID, "nimg out of range");
+  hipStream_t s = (hipStream_t)stream;
+  const size_t ds = dsize(C->dtype);
+  RET(ensure(C->op_imgT, (size_t)nimg * C->npix * ds));
+  const dim3 tg = tile_grid(C, nimg);
+  if (C->dtype == ADMM_DTYPE_F32) {
+    hipLaunchKernelGGL(k_transpose<float>, tg, dim3(kBlock), 0, s, (const float*)img, (float*)C->op_imgT.p, C->g.N);
+    CHECK_LAUNCH();
+    return launch_fwd<float, 0>(C, (const float*)img, (const float*)C->op_imgT.p, (float*)sino, nullptr, nullptr,
+                                nimg, s);
+  }
+  hipLaunchKernelGGL(k_transpose<double>, tg, dim3(kBlock), 0, s, (const double*)img, (double*)C->op_imgT.p,
+                     C->g.N);
+  CHECK_LAUNCH();
+  return launch_fwd<double, 0>(C, (const double*)img, (const double*)C->op_imgT.p, (double*)sino, nullptr, nullptr,
+                               nimg, s);
+}
+
+int admm_project_adj(admm_ctx* C, const void* sino, void* img, int nimg, void* stream) {
+  if (!C || !img || !sino) return fail(ADMM_E_INVALID, "null argument");
+  if (nimg < 1 || nimg > C->max_images) return fail(ADMM_E_INVALID, "nimg out of range");
+  hipStream_t s = (hipStream_t)stream;
+  if (C->dtype == ADMM_DTYPE_F32) {
+    BackArgs<float> a{};
+    a.sino = (const float*)sino;
+    a.out_t = (float*)img;
+    return launch_back<float, BACK_PLAIN>(C, a, nimg, s);
+  }
+  BackArgs<double> a{};
+  a.sino = (const double*)sino;
+  a.out_t = (double*)img;
+  return launch_back<double, BACK_PLAIN>(C, a, nimg, s);
+}
+
+int admm_column_norms_sq(admm_ctx* C, double* W, void* stream) {
+  if (!C || !W) return fail(ADMM_E_INVALID, "null argument");
+  hipStream_t s = (hipStream_t)stream;
+  if (C->dtype == ADMM_DTYPE_F32) {
+    BackArgs<float> a{};
+    a.out_d = W;
+    return launch_back<float, BACK_WSQ>(C, a, 1, s);
+  }
+  BackArgs<double> a{};
+  a.out_d = W;
+  return launch_back<double, BACK_WSQ>(C, a, 1, s);
+}
+
+int admm_tv_grad(admm_ctx* C, const double* x, double* gx, double* gy, int nimg, void* stream) {
+  if (!C || !x || !gx || !gy || nimg < 1) return fail(ADMM_E_INVALID, "bad argument");
+  const int N = C->g.N;
+  hipLaunchKernelGGL(k_tv_grad, dim3((N + 63) / 64, (N + 3) / 4, nimg), dim3(kBlock), 0, (hipStream_t)stream, x,
+                     gx, gy, N);
+  CHECK_LAUNCH();
+  return ADMM_OK;
+}
+
+int admm_tv_div(admm_ctx* C, const double* px, const double* py, double* out, int nimg, void* stream) {
+  if (!C || !px || !py || !out || nimg < 1) return fail(ADMM_E_INVALID, "bad argument");
+  const int N = C->g.N;
+  hipLaunchKernelGGL(k_tv_div, dim3((N + 63) / 64, (N + 3) / 4, nimg), dim3(kBlock), 0, (hipStream_t)stream, px,
+                     py, out, N);
+  CHECK_LAUNCH();
+  return ADMM_OK;
+}
+
+int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
+  if (!C || !batch) return fail(ADMM_E_INVALID, "null argument");
+  const admm_batch& B = *batch;
+  if (B.V < 1) return fail(ADMM_E_INVALID, "batch V < 1");
+  if (B.n_xext < B.V) return fail(ADMM_E_INVALID, "n_xext < V");
+  if (B.tv_iters < 1 || B.cg_iters < 1) return fail(ADMM_E_INVALID, "tv_iters and cg_iters must be >= 1");
+  if (B.tv_kind != ADMM_TV_ISO && B.tv_kind != ADMM_TV_ANISO) return fail(ADMM_E_INVALID, "bad tv_kind");
+  if (!(B.mu > 0)) return fail(ADMM_E_INVALID, "mu must be > 0");
+  if (!B.x_ext || !B.d || !B.e || !B.atb || !B.dsum || !B.b || !B.inc_off || !B.node_stats)
+    return fail(ADMM_E_INVALID, "null batch pointer");
+  if (B.n_edges > 0 && (!B.y || !B.z || !B.q || !B.edge_a || !B.edge_b || !B.inc_edge || !B.inc_qslot ||
+                        !B.inc_sign || !B.edge_stats))
+    return fail(ADMM_E_INVALID, "null edge pointer");
+  if (B.n_edges > 65535) return fail(ADMM_E_INVALID, "more than 65535 edge slots on one device");
+  const size_t npix = C->npix, m = C->mrays;
+  if ((size_t)B.V * npix * 8 >= (1ull << 31) || (size_t)B.V * m * 8 >= (1ull << 31))
+    return fail(ADMM_E_INVALID, "batch too large for 32-bit buffer offsets");
+  HIPCHK(hipSetDevice(C->device));
+  HIPCHK(hipDeviceSynchronize());
+  RET(free_graphs(C));
+  C->b = B;
+  const int V = B.V;
+  const size_t ds = dsize(C->dtype);
+  RET(ensure(C->xs, V * npix * ds));
+  RET(ensure(C->xsT, V * npix * ds));
+  RET(ensure(C->p, V * npix * ds));
+  RET(ensure(C->pT, V * npix * ds));
+  RET(ensure(C->Hp, V * npix * ds));
+  RET(ensure(C->sino, V * m * ds));
+  RET(ensure(C->r, V * npix * 8));
+  RET(ensure(C->c, V * npix * 8));
+  RET(ensure(C->d2, 2 * V * npix * 8));
+  RET(ensure(C->e2, 2 * V * npix * 8));
+  C->P_back = back_partitions(C);
+  const int N = C->g.N;
+  C->P_tile = ((N + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
+  C->P_fwd = ((C->g.n_det + kFwdRays - 1) / kFwdRays) * C->g.n_angles;
+  C->P_edge = (int)((npix + kBlock * 4 - 1) / (kBlock * 4));
+  RET(ensure(C->partH, (size_t)3 * V * C->P_back * 8));
+  RET(ensure(C->partRR, (size_t)V * std::max(C->P_back, C->P_tile) * 8));
+  RET(ensure(C->partS, (size_t)V * C->P_fwd * 8));
+  RET(ensure(C->partD, (size_t)4 * V * C->P_back * 8));
+  RET(ensure(C->partE, (size_t)3 * std::max(1, B.n_edges) * C->P_edge * 8));
+  RET(ensure(C->redH, (size_t)3 * V * 8));
+  RET(ensure(C->rrslot, (size_t)(B.tv_iters * B.cg_iters + 1) * V * 8));
+  C->bound = true;
+  if (C->use_graph) {
+    auto fu = [&](hipStream_t s) {
+      return C->dtype == ADMM_DTYPE_F32 ? enqueue_update<float>(C, s) : enqueue_update<double>(C, s);
+    };
+    RET(capture(C, fu, &C->g_update, &C->x_update));
+    if (B.n_edges > 0) {
+      auto fc = [&](hipStream_t s) { return enqueue_consensus(C, s); };
+      RET(capture(C, fc, &C->g_cons, &C->x_cons));
+    }
+  }
+  HIPCHK(hipDeviceSynchronize());
+  return ADMM_OK;
+}
+
+int admm_batch_atb(admm_ctx* C, double* atb_out, void* stream) {
+  if (!C || !C->bound) return fail(ADMM_E_STATE, "no batch bound");
+  if (!atb_out) return fail(ADMM_E_INVALID, "null atb_out");
+  hipStream_t s = (hipStream_t)stream;
+  if (C->dtype == ADMM_DTYPE_F32) {
+    BackArgs<float> a{};
+    a.sino = (const float*)C->b.b;
+    a.out_d = atb_out;
+    return launch_back<float, BACK_ATB>(C, a, C->b.V, s);
+  }
+  BackArgs<double> a{};
+  a.sino = (const double*)C->b.b;
+  a.out_d = atb_out;
+  return launch_back<double, BACK_ATB>(C, a, C->b.V, s);
+}
+
+int admm_node_update(admm_ctx* C, void* stream) {
+  if (!C || !C->bound) return fail(ADMM_E_STATE, "no batch bound");
+  hipStream_t s = (hipStream_t)stream;
+  if (C->x_update) {
+    HIPCHK(hipGraphLaunch(C->x_update, s));
+    return ADMM_OK;
+  }
+  return C->dtype == ADMM_DTYPE_F32 ? enqueue_update<float>(C, s) : enqueue_update<double>(C, s);
+}
+
+int admm_consensus(admm_ctx* C, void* stream) {
+  if (!C || !C->bound) return fail(ADMM_E_STATE, "no batch bound");
+  hipStream_t s = (hipStream_t)stream;
+  if (C->x_cons) {
+    HIPCHK(hipGraphLaunch(C->x_cons, s));
+    return ADMM_OK;
+  }
+  return enqueue_consensus(C, s);
+}
+
+int admm_time_forward(admm_ctx* C, int reps, void* stream, double* ms_out) {
+  if (!C || !C->bound) return fail(ADMM_E_STATE, "no batch bound");
+  if (reps < 1 || !ms_out) return fail(ADMM_E_INVALID, "bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  // warm-up
+  if (C->dtype == ADMM_DTYPE_F32)
+    RET((launch_fwd<float, 0>(C, (float*)C->xs.p, (float*)C->xsT.p, (float*)C->sino.p, nullptr, nullptr, C->b.V, s)));
+  else
+    RET((launch_fwd<double, 0>(C, (double*)C->xs.p, (double*)C->xsT.p, (double*)C->sino.p, nullptr, nullptr, C->b.V,
+                               s)));
+  HIPCHK(hipEventRecord(e0, s));
+  for (int i = 0; i < reps; ++i) {
+    if (C->dtype == ADMM_DTYPE_F32)
+      RET((launch_fwd<float, 0>(C, (float*)C->xs.p, (float*)C->xsT.p, (float*)C->sino.p, nullptr, nullptr, C->b.V,
+                                s)));
+    else
+      RET((launch_fwd<double, 0>(C, (double*)C->xs.p, (double*)C->xsT.p, (double*)C->sino.p, nullptr, nullptr,
+                                 C->b.V, s)));
+  }
+  HIPCHK(hipEventRecord(e1, s));
+  HIPCHK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  *ms_out = (double)ms / reps;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return ADMM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,735 @@
+// kernels.hpp -- CDNA4 (gfx950) kernels of the decentralized-ADMM tomography hot path.
+//
+// Everything is batched over the graph nodes this GPU owns ("node batch"):
+// all nodes share one parallel-beam geometry (block_2_load_odl_data.py:51,
+// every node spans [0, pi) with its own a angles), so one launch projects
+// VB node images at once and the per-step geometry (interpolation position,
+// weights, clamped offsets) is computed once and reused VB times.
+//
+// Numerics (see DESIGN.md "Numerics"):
+//   * projector inputs/outputs ("samples") are T = float (C2-C4) or double (C5);
+//   * interpolation positions are evaluated in float64 so the operator matches
+//     the float64 oracle to ~1e-7 (a float32 position has 3e-5 absolute error at N=512);
+//   * the CG solution x, residual r, split-Bregman d/e and edge state y/z are float64;
+//   * every reduction is a fixed-order tree over fixed partial slots:
+//     bitwise reproducible, independent of how many GPUs hold the graph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace admm {
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+constexpr int kTile = 64;        // elementwise / transposing kernels: 64x64 pixel tiles
+constexpr int kBackTileJ = 64;   // back-projector block: 64 (j) x 4 (i) pixels
+constexpr int kBackTileI = 4;
+constexpr int kFwdRays = 64;     // forward-projector block: 64 rays x 4 step segments
+constexpr int kFwdSegs = 4;
+constexpr int kAngChunk = 256;   // back-projector angle table chunk staged in LDS
+
+// Per-angle forward-projector constants (host-computed in float64).
+// Ray (t,k), step m:  l = A0 + k*A1 + m*dl  (interpolation coordinate).
+struct FwdAngle {
+  double A0, A1, dl;
+  float L;    // path length per step h/|alpha|
+  int caseA;  // 1: step over axis-1 index on the transposed image
+};
+// Per-angle back-projector constants: fractional bin k_f = B0 + i*Bi + j*Bj,
+// weight(k) = max(0, 1 - |k-k_f|*slope) * L.
+struct BackAngle {
+  double B0, Bi, Bj;
+  float slope, L;
+};
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
+
+// ---------------------------------------------------------------------------
+// buffer loads: one 128-bit resource per array, 32-bit per-lane byte offsets,
+// per-node offsets in an SGPR (soffset) -> no per-lane 64-bit address math.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ T bload(__amdgpu_buffer_rsrc_t r, int voff, int soff);
+template <>
+__device__ __forceinline__ float bload<float>(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+template <>
+__device__ __forceinline__ double bload<double>(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+
+// ---------------------------------------------------------------------------
+// deterministic block reduction of NQ float64 values per thread (256 threads)
+// result valid in thread 0.  Fixed shuffle tree + fixed LDS order.
+// ---------------------------------------------------------------------------
+template <int NQ>
+__device__ __forceinline__ void block_reduce(double (&v)[NQ], double* lds /* >= 4*NQ */) {
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    double s = v[q];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+    v[q] = s;
+  }
+  const int wid = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) lds[wid * NQ + q] = v[q];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) v[q] = ((lds[q] + lds[NQ + q]) + (lds[2 * NQ + q] + lds[3 * NQ + q]));
+  }
+  __syncthreads();
+}
+
+// ===========================================================================
+// Forward projector (Joseph, ray-driven):  sino[v][t][k] = sum_m L * interp(img_v, row m, l(m))
+// Replaces the ODL RayTransform `Ai @ x` (block_2_load_odl_data.py:72, dense form :86-114;
+// used at block_5_node_problem.py:21 and block_6_admm_loop_ver2.py:193).
+//
+// Block = 64 consecutive detector bins of one angle x 4 step segments (one wave each).
+// Lanes are consecutive rays, so at every step a wave reads one contiguous row segment:
+// case-B angles read img (row m = axis-0 index), case-A angles read the transposed
+// copy imgT (row m = axis-1 index) -- both coalesced.  The 4 segment partial sums
+// are combined in LDS in fixed order.
+// MODE 0: store A x.   MODE 1: store s = A x - b and per-block partials of ||s||^2.
+// ===========================================================================
+template <typename T, int VB, int MODE>
+__global__ __launch_bounds__(kBlock) void k_fwd(const T* __restrict__ img, const T* __restrict__ imgT,
+                                                T* __restrict__ sino, const T* __restrict__ bsino,
+                                                double* __restrict__ part, const FwdAngle* __restrict__ ang,
+                                                int N, int n_det, int n_ang, int V) {
+  const int lane = threadIdx.x & 63;
+  const int seg = threadIdx.x >> 6;
+  const int k = blockIdx.x * kFwdRays + lane;
+  const int t = blockIdx.y;
+  const int v0 = blockIdx.z * VB;
+  const int nv = min(VB, V - v0);
+  const int npix = N * N;
+  const FwdAngle a = ang[t];
+  const T* src = a.caseA ? imgT : img;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(src, (uint32_t)((size_t)V * npix * sizeof(T)));
+  T acc[VB];
+#pragma unroll
+  for (int u = 0; u < VB; ++u) acc[u] = T(0);
+
+  if (k < n_det) {
+    const double l0 = fma((double)k, a.A1, a.A0);
+    // steps whose interpolation coordinate lies in (-1, N); conservative, taps are predicated
+    int mlo = 0, mhi = N - 1;
+    if (fabs(a.dl) > 1e-12) {
+      double ma = (-1.0 - l0) / a.dl, mb = ((double)N - l0) / a.dl;
+      double lo = fmax(fmin(ma, mb), -1.0), hi = fmin(fmax(ma, mb), (double)N);
+      mlo = max(0, (int)floor(lo));
+      mhi = min(N - 1, (int)ceil(hi));
+    } else if (!(l0 > -1.0 && l0 < (double)N)) {
+      mlo = 1;
+      mhi = 0;
+    }
+    const int segLen = (N + kFwdSegs - 1) / kFwdSegs;
+    const int s0 = max(mlo, seg * segLen);
+    const int s1 = min(mhi, seg * segLen + segLen - 1);
+    for (int m = s0; m <= s1; ++m) {
+      const double l = fma((double)m, a.dl, l0);
+      const double fl = floor(l);
+      const int i0 = (int)fl;
+      T w1 = (T)(l - fl);
+      T w0 = T(1) - w1;
+      w0 = (i0 >= 0 && i0 <= N - 1) ? w0 : T(0);
+      w1 = (i0 >= -1 && i0 <= N - 2) ? w1 : T(0);
+      const int row = m * N;
+      const int o0 = (row + clampi(i0, 0, N - 1)) * (int)sizeof(T);
+      const int o1 = (row + clampi(i0 + 1, 0, N - 1)) * (int)sizeof(T);
+#pragma unroll
+      for (int u = 0; u < VB; ++u) {
+        if (u < nv) {
+          const int so = (v0 + u) * npix * (int)sizeof(T);
+          const T p0 = bload<T>(rs, o0, so);
+          const T p1 = bload<T>(rs, o1, so);
+          acc[u] = fma(w0, p0, acc[u]);
+          acc[u] = fma(w1, p1, acc[u]);
+        }
+      }
+    }
+  }
+  __shared__ T red[kFwdSegs][VB][kFwdRays];
+#pragma unroll
+  for (int u = 0; u < VB; ++u) red[seg][u][lane] = acc[u];
+  __syncthreads();
+  double sq[VB];
+#pragma unroll
+  for (int u = 0; u < VB; ++u) sq[u] = 0.0;
+  if (seg == 0 && k < n_det) {
+#pragma unroll
+    for (int u = 0; u < VB; ++u) {
+      if (u < nv) {
+        T s = ((red[0][u][lane] + red[1][u][lane]) + (red[2][u][lane] + red[3][u][lane])) * (T)a.L;
+        const size_t o = (size_t)(v0 + u) * n_ang * n_det + (size_t)t * n_det + k;
+        if (MODE == 1) {
+          s = s - bsino[o];
+          sq[u] = (double)s * (double)s;
+        }
+        sino[o] = s;
+      }
+    }
+  }
+  if (MODE == 1) {
+    __syncthreads();
+    __shared__ double lds[4 * VB];
+    block_reduce<VB>(sq, lds);
+    if (threadIdx.x == 0) {
+      const int P = gridDim.x * gridDim.y;
+      const int b = blockIdx.y * gridDim.x + blockIdx.x;
+#pragma unroll
+      for (int u = 0; u < VB; ++u)
+        if (u < nv) part[(size_t)(v0 + u) * P + b] = sq[u];
+    }
+  }
+}
+
+// ===========================================================================
+// Back projector (pixel-driven gather; exact transpose of the Joseph weights):
+//   acc[v][i,j] = sum_t sum_{k in {k0,k0+1}} w_t(k) * sino[v][t][k]
+// Replaces `Ai.T @ r` (block_6_admm_loop_ver2.py:145).  No atomics: each pixel
+// gathers its <= 2 bins per angle.  The angle table is staged in LDS.
+// Fused epilogues (MODE):
+//   BACK_PLAIN : out = A^T s                                   (operator API)
+//   BACK_ATB   : atb = A^T b (float64)                          (setup)
+//   BACK_WSQ   : W = max(sum_r A[r,p]^2, 1e-12) (float64)       (make_precisions, block_3:20-23)
+//   BACK_H     : Hp = A^T A p + rho D p + mu K^T K p; partials p.Hp, r.Hp, Hp.Hp  (CG)
+//   BACK_INIT  : r = A^T b + rho c + mu K^T(d-e) - H xs;  p = r; partial r.r   (CG start)
+//   BACK_DIAG  : g = A^T s + rho (D x - c) + lam K^T sub(Kx); partials |g|^2, TV(x),
+//                sum_j rho/2 q_ij (x - v_ij)^2, |x - phantom|^2   (block_6_ver2.py:135-149)
+// ===========================================================================
+enum BackMode { BACK_PLAIN = 0, BACK_ATB = 1, BACK_WSQ = 2, BACK_H = 3, BACK_INIT = 4, BACK_DIAG = 5 };
+
+template <typename T>
+struct BackArgs {
+  const T* sino;            // [V][m]
+  const BackAngle* ang;     // [n_ang]
+  int N, n_det, n_ang, V;
+  // outputs
+  T* out_t;                 // PLAIN: [V][n];  H: Hp [V][n];  INIT: p [V][n]
+  double* out_d;            // ATB: atb;  WSQ: W;  INIT: r
+  double* part;             // [V][NQ][P]
+  // epilogue inputs
+  const T* pin;             // H: p;  INIT: xs (sample copy of x)
+  const double* r;          // H: r (float64 residual)
+  const double* dsum;       // [V][n]
+  const double* atb;        // INIT
+  const double* cvec;       // INIT, DIAG: c = sum_j q v
+  const double* dvar;       // INIT: d [V][2][n]
+  const double* evar;       // INIT: e [V][2][n]
+  const double* x;          // DIAG: x rows of x_ext
+  const double* phantom;    // DIAG (may be null)
+  const double* yv;         // DIAG: edge y [E][n]
+  const double* zv;         // DIAG: edge z [E][n]
+  const double* qv;         // DIAG: q slots
+  const int* inc_off;       // DIAG
+  const int* inc_edge;
+  const int* inc_qslot;
+  const int* inc_sign;
+  double rho, lam, mu;
+  int tv_kind;
+};
+
+// forward difference at (i,j) of a float64 image (zero at the last row / column)
+__device__ __forceinline__ void grad_at(const double* __restrict__ x, int N, int i, int j, double& gx, double& gy) {
+  const double c = x[i * N + j];
+  gx = (i < N - 1) ? x[(i + 1) * N + j] - c : 0.0;
+  gy = (j < N - 1) ? x[i * N + j + 1] - c : 0.0;
+}
+
+// TV subgradient direction at a gradient (block_4_tv_helpers.py:37-46, eps = 1e-12)
+__device__ __forceinline__ void tv_sub(double gx, double gy, int kind, double& px, double& py) {
+  if (kind == 0) {
+    const double m = sqrt(gx * gx + gy * gy);
+    if (m > 1e-12) {
+      px = gx / m;
+      py = gy / m;
+    } else {
+      px = 0.0;
+      py = 0.0;
+    }
+  } else {
+    px = fabs(gx) > 1e-12 ? copysign(1.0, gx) : 0.0;
+    py = fabs(gy) > 1e-12 ? copysign(1.0, gy) : 0.0;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ double ktk_at(const T* __restrict__ p, int N, int i, int j) {
+  // (K^T K p)[i,j] with Neumann (zero last-difference) boundary
+  const double c = (double)p[i * N + j];
+  double s = 0.0;
+  if (i >= 1) s += c - (double)p[(i - 1) * N + j];
+  if (i <= N - 2) s -= (double)p[(i + 1) * N + j] - c;
+  if (j >= 1) s += c - (double)p[i * N + j - 1];
+  if (j <= N - 2) s -= (double)p[i * N + j + 1] - c;
+  return s;
+}
+
+// (K^T w)[i,j] for a two-component float64 field w = d - e stored [2][n]
+__device__ __forceinline__ double kt_w_at(const double* __restrict__ d, const double* __restrict__ e, int N,
+                                          int i, int j) {
+  const int n = N * N;
+  double s = 0.0;
+  const int o = i * N + j;
+  if (i >= 1) s += d[o - N] - e[o - N];
+  if (i <= N - 2) s -= d[o] - e[o];
+  if (j >= 1) s += d[n + o - 1] - e[n + o - 1];
+  if (j <= N - 2) s -= d[n + o] - e[n + o];
+  return s;
+}
+
+template <typename T, int VB, int MODE>
+__global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
+  constexpr int NQ = (MODE == BACK_H) ? 3 : (MODE == BACK_INIT) ? 1 : (MODE == BACK_DIAG) ? 4 : 1;
+  const int N = A.N, n_det = A.n_det, n_ang = A.n_ang;
+  const int npix = N * N;
+  const int m_rays = n_ang * n_det;
+  const int j = blockIdx.x * kBackTileJ + (threadIdx.x & 63);
+  const int i = blockIdx.y * kBackTileI + (threadIdx.x >> 6);
+  const bool inb = (i < N) && (j < N);
+  const int v0 = blockIdx.z * VB;
+  const int nv = (MODE == BACK_WSQ) ? 1 : min(VB, A.V - v0);
+  const __amdgpu_buffer_rsrc_t rs =
+      make_rsrc(A.sino, (uint32_t)((size_t)A.V * m_rays * sizeof(T)));
+
+  __shared__ BackAngle sang[kAngChunk];
+  T acc[VB];
+#pragma unroll
+  for (int u = 0; u < VB; ++u) acc[u] = T(0);
+  const double di = (double)i, dj = (double)j;
+
+  for (int t0 = 0; t0 < n_ang; t0 += kAngChunk) {
+    const int nt = min(kAngChunk, n_ang - t0);
+    __syncthreads();
+    for (int q = threadIdx.x; q < nt; q += kBlock) sang[q] = A.ang[t0 + q];
+    __syncthreads();
+    if (inb) {
+      for (int tt = 0; tt < nt; ++tt) {
+        const BackAngle g = sang[tt];
+        const double kf = fma(di, g.Bi, fma(dj, g.Bj, g.B0));
+        const double kfl = floor(kf);
+        const int k0 = (int)kfl;
+        const T f = (T)(kf - kfl);
+        T w0 = fmax(T(0), T(1) - f * (T)g.slope) * (T)g.L;
+        T w1 = fmax(T(0), T(1) - (T(1) - f) * (T)g.slope) * (T)g.L;
+        w0 = (k0 >= 0 && k0 <= n_det - 1) ? w0 : T(0);
+        w1 = (k0 >= -1 && k0 <= n_det - 2) ? w1 : T(0);
+        if (MODE == BACK_WSQ) {
+          acc[0] = fma(w0, w0, acc[0]);
+          acc[0] = fma(w1, w1, acc[0]);
+        } else {
+          const int rowo = (t0 + tt) * n_det;
+          const int o0 = (rowo + clampi(k0, 0, n_det - 1)) * (int)sizeof(T);
+          const int o1 = (rowo + clampi(k0 + 1, 0, n_det - 1)) * (int)sizeof(T);
+#pragma unroll
+          for (int u = 0; u < VB; ++u) {
+            if (u < nv) {
+              const int so = (v0 + u) * m_rays * (int)sizeof(T);
+              const T s0 = bload<T>(rs, o0, so);
+              const T s1 = bload<T>(rs, o1, so);
+              acc[u] = fma(w0, s0, acc[u]);
+              acc[u] = fma(w1, s1, acc[u]);
+            }
+          }
+        }
+      }
+    }
+  }
+
+  // ---------------- fused epilogues ----------------
+  const int pix = i * N + j;
+  if (MODE == BACK_PLAIN) {
+    if (inb) {
+#pragma unroll
+      for (int u = 0; u < VB; ++u)
+        if (u < nv) A.out_t[(size_t)(v0 + u) * npix + pix] = acc[u];
+    }
+    return;
+  }
+  if (MODE == BACK_ATB) {
+    if (inb) {
+#pragma unroll
+      for (int u = 0; u < VB; ++u)
+        if (u < nv) A.out_d[(size_t)(v0 + u) * npix + pix] = (double)acc[u];
+    }
+    return;
+  }
+  if (MODE == BACK_WSQ) {
+    if (inb) A.out_d[pix] = fmax((double)acc[0], 1e-12);
+    return;
+  }
+
+  double pq[VB][NQ];
+#pragma unroll
+  for (int u = 0; u < VB; ++u)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) pq[u][q] = 0.0;
+
+  if (inb) {
+#pragma unroll
+    for (int u = 0; u < VB; ++u) {
+      if (u >= nv) continue;
+      const int v = v0 + u;
+      const size_t vo = (size_t)v * npix;
+      if (MODE == BACK_H || MODE == BACK_INIT) {
+        const T* pv = A.pin + vo;
+        const double pc = (double)pv[pix];
+        const double h = (double)acc[u] + A.rho * A.dsum[vo + pix] * pc + A.mu * ktk_at<T>(pv, N, i, j);
+        if (MODE == BACK_H) {
+          const T hp = (T)h;
+          A.out_t[vo + pix] = hp;
+          const double hd = (double)hp;
+          pq[u][0] = pc * hd;
+          pq[u][1] = A.r[vo + pix] * hd;
+          pq[u][2] = hd * hd;
+        } else {
+          const double* dv = A.dvar + 2 * vo;
+          const double* ev = A.evar + 2 * vo;
+          const double rr = A.atb[vo + pix] + A.rho * A.cvec[vo + pix] + A.mu * kt_w_at(dv, ev, N, i, j) - h;
+          A.out_d[vo + pix] = rr;
+          A.out_t[vo + pix] = (T)rr;
+          pq[u][0] = rr * rr;
+        }
+      } else if (MODE == BACK_DIAG) {
+        const double* xv = A.x + vo;
+        const double xc = xv[pix];
+        // lam * K^T sub(Kx) at (i,j): needs the subgradient at (i,j), (i-1,j), (i,j-1)
+        double gx, gy, px, py, kts = 0.0, tvv;
+        grad_at(xv, N, i, j, gx, gy);
+        tv_sub(gx, gy, A.tv_kind, px, py);
+        tvv = (A.tv_kind == 0) ? sqrt(gx * gx + gy * gy) : fabs(gx) + fabs(gy);
+        if (i <= N - 2) kts -= px;
+        if (j <= N - 2) kts -= py;
+        if (i >= 1) {
+          double ax, ay, bx, by;
+          grad_at(xv, N, i - 1, j, ax, ay);
+          tv_sub(ax, ay, A.tv_kind, bx, by);
+          kts += bx;
+        }
+        if (j >= 1) {
+          double ax, ay, bx, by;
+          grad_at(xv, N, i, j - 1, ax, ay);
+          tv_sub(ax, ay, A.tv_kind, bx, by);
+          kts += by;
+        }
+        const double cc = A.cvec[vo + pix];
+        const double g = (double)acc[u] + A.rho * (A.dsum[vo + pix] * xc - cc) + A.lam * kts;
+        double quad = 0.0;
+        for (int q = A.inc_off[v]; q < A.inc_off[v + 1]; ++q) {
+          const size_t eo = (size_t)A.inc_edge[q] * npix + pix;
+          const double vij = A.zv[eo] - (double)A.inc_sign[q] * A.yv[eo];
+          const double dd = xc - vij;
+          quad += A.qv[(size_t)A.inc_qslot[q] * npix + pix] * dd * dd;
+        }
+        pq[u][0] = g * g;
+        pq[u][1] = tvv;
+        pq[u][2] = 0.5 * A.rho * quad;
+        if (A.phantom) {
+          const double dp = xc - A.phantom[pix];
+          pq[u][3] = dp * dp;
+        }
+      }
+    }
+  }
+  __shared__ double lds[4 * VB * NQ];
+  double flat[VB * NQ];
+#pragma unroll
+  for (int u = 0; u < VB; ++u)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) flat[u * NQ + q] = pq[u][q];
+  block_reduce<VB * NQ>(flat, lds);
+  if (threadIdx.x == 0) {
+    const int P = gridDim.x * gridDim.y;
+    const int b = blockIdx.y * gridDim.x + blockIdx.x;
+#pragma unroll
+    for (int u = 0; u < VB; ++u)
+      if (u < nv)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) A.part[((size_t)(v0 + u) * NQ + q) * P + b] = flat[u * NQ + q];
+  }
+}
+
+// ===========================================================================
+// 64x64-tile elementwise kernels (block 256 = 64 x 4, 16 rows per thread).
+// Each writes its "sample" output both row-major and transposed (LDS tile),
+// because the forward projector reads the transposed copy for case-A angles.
+// ===========================================================================
+template <typename T>
+__device__ __forceinline__ void tile_store_T(T (&tl)[kTile][kTile + 1], T* __restrict__ outT, int N, int i0,
+                                             int j0) {
+  __syncthreads();
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  // outT[j][i] = tile[i-i0][j-j0]
+  for (int r = ty; r < kTile; r += 4) {
+    const int jj = j0 + r, ii = i0 + tx;
+    if (jj < N && ii < N) outT[(size_t)jj * N + ii] = tl[tx][r];
+  }
+}
+
+// gather (prologue of the x-update, block_6_admm_loop_ver2.py:85-95,137-140):
+//   c_v = sum_{e in inc(v)} q_e (z_e - sign * y_e);  xs = (T) x, xsT = xs^T
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_gather(const double* __restrict__ x, const double* __restrict__ y,
+                                                   const double* __restrict__ z, const double* __restrict__ q,
+                                                   const int* __restrict__ inc_off, const int* __restrict__ inc_edge,
+                                                   const int* __restrict__ inc_qslot,
+                                                   const int* __restrict__ inc_sign, double* __restrict__ c,
+                                                   T* __restrict__ xs, T* __restrict__ xsT, int N) {
+  __shared__ T tl[kTile][kTile + 1];
+  const int v = blockIdx.z;
+  const int npix = N * N;
+  const int i0 = blockIdx.y * kTile, j0 = blockIdx.x * kTile;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int e0 = inc_off[v], e1 = inc_off[v + 1];
+  const size_t vo = (size_t)v * npix;
+  for (int r = ty; r < kTile; r += 4) {
+    const int i = i0 + r, j = j0 + tx;
+    if (i < N && j < N) {
+      const int pix = i * N + j;
+      double acc = 0.0;
+      for (int qq = e0; qq < e1; ++qq) {
+        const size_t eo = (size_t)inc_edge[qq] * npix + pix;
+        const double vij = z[eo] - (double)inc_sign[qq] * y[eo];
+        acc += q[(size_t)inc_qslot[qq] * npix + pix] * vij;
+      }
+      c[vo + pix] = acc;
+      const T s = (T)x[vo + pix];
+      xs[vo + pix] = s;
+      tl[r][tx] = s;
+    }
+  }
+  tile_store_T<T>(tl, xsT + vo, N, i0, j0);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_transpose(const T* __restrict__ in, T* __restrict__ outT, int N) {
+  __shared__ T tl[kTile][kTile + 1];
+  const int v = blockIdx.z;
+  const size_t vo = (size_t)v * N * N;
+  const int i0 = blockIdx.y * kTile, j0 = blockIdx.x * kTile;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < kTile; r += 4) {
+    const int i = i0 + r, j = j0 + tx;
+    if (i < N && j < N) tl[r][tx] = in[vo + (size_t)i * N + j];
+  }
+  tile_store_T<T>(tl, outT + vo, N, i0, j0);
+}
+
+// CG step with the single-reduction identity (see oracle/node_solver.py):
+//   alpha = rr/pHp, rr' = rr - 2 alpha rHp + alpha^2 HpHp, beta = rr'/rr
+//   x += alpha p;  r -= alpha Hp;  p = r + beta p  (p also written transposed)
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_cg_update(double* __restrict__ x, double* __restrict__ r,
+                                                      T* __restrict__ p, T* __restrict__ pT,
+                                                      const T* __restrict__ Hp, const double* __restrict__ redH,
+                                                      const double* __restrict__ rr_in, double* __restrict__ rr_out,
+                                                      int N) {
+  __shared__ T tl[kTile][kTile + 1];
+  const int v = blockIdx.z;
+  const double pHp = redH[3 * v + 0], rHp = redH[3 * v + 1], HH = redH[3 * v + 2];
+  const double rr = rr_in[v];
+  const double alpha = (pHp != 0.0) ? rr / pHp : 0.0;
+  double rrn = rr - 2.0 * alpha * rHp + alpha * alpha * HH;
+  rrn = fmax(rrn, 0.0);
+  const double beta = (rr != 0.0) ? rrn / rr : 0.0;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) rr_out[v] = rrn;
+  const size_t vo = (size_t)v * N * N;
+  const int i0 = blockIdx.y * kTile, j0 = blockIdx.x * kTile;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int rw = ty; rw < kTile; rw += 4) {
+    const int i = i0 + rw, j = j0 + tx;
+    if (i < N && j < N) {
+      const size_t o = vo + (size_t)i * N + j;
+      const double pv = (double)p[o];
+      const double hv = (double)Hp[o];
+      x[o] += alpha * pv;
+      const double rn = r[o] - alpha * hv;
+      r[o] = rn;
+      const T np = (T)(rn + beta * pv);
+      p[o] = np;
+      tl[rw][tx] = np;
+    }
+  }
+  tile_store_T<T>(tl, pT + vo, N, i0, j0);
+}
+
+// split-Bregman (d, e) update after a CG solve:
+//   u = Kx + e, d' = shrink(u, lam/mu), e' = u - d'
+// and, unless LAST, the residual shift r += mu K^T((d'-e') - (d-e)), restart p = r,
+// partial r.r.  With LAST the sample copy xs = (T) x (+ transpose) is produced for
+// the diagnostics epilogue instead.  d/e are ping-ponged (din -> dout) because the
+// stencil reads neighbours' old values.
+__device__ __forceinline__ void shrink2(double ux, double uy, double tau, int kind, double& dx, double& dy) {
+  if (kind == 0) {
+    const double s = sqrt(ux * ux + uy * uy);
+    const double f = (s > tau) ? (s - tau) / s : 0.0;
+    dx = f * ux;
+    dy = f * uy;
+  } else {
+    dx = copysign(fmax(fabs(ux) - tau, 0.0), ux);
+    dy = copysign(fmax(fabs(uy) - tau, 0.0), uy);
+  }
+}
+
+template <typename T, bool LAST>
+__global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__ x, const double* __restrict__ din,
+                                                      const double* __restrict__ ein, double* __restrict__ dout,
+                                                      double* __restrict__ eout, double* __restrict__ r,
+                                                      T* __restrict__ p, T* __restrict__ pT,
+                                                      double* __restrict__ part, double tau, double mu, int kind,
+                                                      int N) {
+  __shared__ T tl[kTile][kTile + 1];
+  __shared__ double lds[4];
+  const int v = blockIdx.z;
+  const int npix = N * N;
+  const size_t vo = (size_t)v * npix;
+  const double* xv = x + vo;
+  const double* dv = din + 2 * vo;
+  const double* ev = ein + 2 * vo;
+  const int i0 = blockIdx.y * kTile, j0 = blockIdx.x * kTile;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  double rrp = 0.0;
+  for (int rw = ty; rw < kTile; rw += 4) {
+    const int i = i0 + rw, j = j0 + tx;
+    if (i >= N || j >= N) continue;
+    const int o = i * N + j;
+    double gx, gy, ux, uy, ndx, ndy;
+    grad_at(xv, N, i, j, gx, gy);
+    ux = gx + ev[o];
+    uy = gy + ev[npix + o];
+    shrink2(ux, uy, tau, kind, ndx, ndy);
+    const double nex = ux - ndx, ney = uy - ndy;
+    dout[2 * vo + o] = ndx;
+    dout[2 * vo + npix + o] = ndy;
+    eout[2 * vo + o] = nex;
+    eout[2 * vo + npix + o] = ney;
+    T s;
+    if (!LAST) {
+      // K^T(dw) at (i,j): dw_x(i-1,j) - dw_x(i,j) + dw_y(i,j-1) - dw_y(i,j)
+      double kt = 0.0;
+      if (i <= N - 2) kt -= (ndx - nex) - (dv[o] - ev[o]);
+      if (j <= N - 2) kt -= (ndy - ney) - (dv[npix + o] - ev[npix + o]);
+      if (i >= 1) {
+        const int oo = o - N;
+        double ax, ay, bx, by;
+        grad_at(xv, N, i - 1, j, ax, ay);
+        const double vx = ax + ev[oo], vy = ay + ev[npix + oo];
+        shrink2(vx, vy, tau, kind, bx, by);
+        kt += (bx - (vx - bx)) - (dv[oo] - ev[oo]);
+      }
+      if (j >= 1) {
+        const int oo = o - 1;
+        double ax, ay, bx, by;
+        grad_at(xv, N, i, j - 1, ax, ay);
+        const double vx = ax + ev[oo], vy = ay + ev[npix + oo];
+        shrink2(vx, vy, tau, kind, bx, by);
+        kt += (by - (vy - by)) - (dv[npix + oo] - ev[npix + oo]);
+      }
+      const double rn = r[vo + o] + mu * kt;
+      r[vo + o] = rn;
+      rrp += rn * rn;
+      s = (T)rn;
+    } else {
+      s = (T)xv[o];
+    }
+    p[vo + o] = s;
+    tl[rw][tx] = s;
+  }
+  tile_store_T<T>(tl, pT + vo, N, i0, j0);
+  if (!LAST) {
+    double a[1] = {rrp};
+    block_reduce<1>(a, lds);
+    if (threadIdx.x == 0) part[(size_t)v * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + blockIdx.x] = a[0];
+  }
+}
+
+// ===========================================================================
+// Consensus / dual / residual kernel, one edge per blockIdx.y
+// (block_6_admm_loop_ver2.py:210-253):
+//   a_a = x_a + y, a_b = x_b - y, z' = (a_a + a_b)/2, y' = y + x_a - z'
+//   partials of |x_a - z'|^2, |x_b - z'|^2, |z' - z|^2
+// ===========================================================================
+__global__ __launch_bounds__(kBlock) void k_consensus(const double* __restrict__ xext, double* __restrict__ y,
+                                                      double* __restrict__ z, const int* __restrict__ ea,
+                                                      const int* __restrict__ eb, double* __restrict__ part,
+                                                      int npix) {
+  __shared__ double lds[12];
+  const int e = blockIdx.y;
+  const size_t eo = (size_t)e * npix;
+  const double* xa = xext + (size_t)ea[e] * npix;
+  const double* xb = xext + (size_t)eb[e] * npix;
+  double acc[3] = {0.0, 0.0, 0.0};
+  const int base = blockIdx.x * (kBlock * 4);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int pix = base + u * kBlock + threadIdx.x;
+    if (pix < npix) {
+      const double xav = xa[pix], xbv = xb[pix], yv = y[eo + pix], zo = z[eo + pix];
+      const double aa = xav + yv, ab = xbv - yv;
+      const double zn = (aa + ab) * 0.5;
+      y[eo + pix] = yv + xav - zn;
+      z[eo + pix] = zn;
+      const double ra = xav - zn, rb = xbv - zn, dz = zn - zo;
+      acc[0] += ra * ra;
+      acc[1] += rb * rb;
+      acc[2] += dz * dz;
+    }
+  }
+  block_reduce<3>(acc, lds);
+  if (threadIdx.x == 0) {
+    const int P = gridDim.x;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) part[((size_t)e * 3 + q) * P + blockIdx.x] = acc[q];
+  }
+}
+
+// rows of P partials -> one value each, fixed order (deterministic).
+// out[(r / G) * ostride + ooff + (r % G)] = sum_p part[r * P + p]
+__global__ __launch_bounds__(kBlock) void k_reduce_rows(const double* __restrict__ part, int P, double* __restrict__ out,
+                                                        int G, int ostride, int ooff) {
+  __shared__ double lds[4];
+  const int r = blockIdx.x;
+  double s = 0.0;
+  for (int p = threadIdx.x; p < P; p += kBlock) s += part[(size_t)r * P + p];
+  double a[1] = {s};
+  block_reduce<1>(a, lds);
+  if (threadIdx.x == 0) out[(size_t)(r / G) * ostride + ooff + (r % G)] = a[0];
+}
+
+// K x and K^T p for the operator API (float64)
+__global__ void k_tv_grad(const double* __restrict__ x, double* __restrict__ gx, double* __restrict__ gy, int N) {
+  const int v = blockIdx.z;
+  const size_t vo = (size_t)v * N * N;
+  const int j = blockIdx.x * 64 + (threadIdx.x & 63), i = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= N || j >= N) return;
+  double a, b;
+  grad_at(x + vo, N, i, j, a, b);
+  gx[vo + i * N + j] = a;
+  gy[vo + i * N + j] = b;
+}
+__global__ void k_tv_div(const double* __restrict__ px, const double* __restrict__ py, double* __restrict__ out,
+                         int N) {
+  const int v = blockIdx.z;
+  const size_t vo = (size_t)v * N * N;
+  const int j = blockIdx.x * 64 + (threadIdx.x & 63), i = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= N || j >= N) return;
+  const int o = i * N + j;
+  double s = 0.0;
+  if (i >= 1) s += px[vo + o - N];
+  if (i <= N - 2) s -= px[vo + o];
+  if (j >= 1) s += py[vo + o - 1];
+  if (j <= N - 2) s -= py[vo + o];
+  out[vo + o] = s;
+}
+
+}  // namespace admm

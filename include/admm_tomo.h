@@ -1,0 +1,168 @@
+/*
+ * admm_tomo.h -- C-ABI of the MI355X-native decentralized-ADMM tomography hot path.
+ *
+ * The reference (prsinha1/Distributed-Inverse-Problem-Admm) is pure Python and
+ * has no FFI.  Its hot-path boundary is two duck-typed Python functions:
+ *
+ *   build_node_problem(Ai, bi, rho, neighbor_terms, N, lam_tv, Qij_terms)
+ *       -> /root/reference/block_5_node_problem.py:6-32
+ *   decentralized_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, ...)
+ *       -> /root/reference/block_6_admm_loop_ver2.py:15-326
+ *          (kwarg surface also of block_6_admm_loop.py:72-84)
+ *
+ * plus the operator they consume, the ODL ray transform materialised as a dense
+ * matrix (block_2_load_odl_data.py:34-114), used only through `A @ x`,
+ * `A.T @ r` and column norms (block_6_admm_loop_ver2.py:145,193;
+ * block_3_graph_and_precisions.py:20-23).  The Python drop-ins in
+ * distributed-inverse-problem-admm_amd/ call the entry points below through
+ * ctypes.  Each entry point names the reference code it replaces.
+ *
+ * Conventions
+ *   - All array arguments are DEVICE pointers owned by the caller (PyTorch
+ *     tensors).  The context owns only geometry tables and scratch.
+ *   - Image layout: node-major, C-order pixels, x[v*N*N + i*N + j] <-> pixel
+ *     (x_i, y_j) of ODL's uniform_discr([-1,-1],[1,1],[N,N]) (axis 0 = x).
+ *   - Sinogram layout: node-major, angle-major: b[v*A*D + t*D + k]
+ *     (block_6_admm_loop_ver2.py:46 flattens the (angles, det) sinogram in C order).
+ *   - "sample" arrays (images given to the projector, sinograms) have the
+ *     context dtype (ADMM_DTYPE_F32 or ADMM_DTYPE_F64); solver state
+ *     (x, d, e, y, z, q, A^T b, sum q) is always float64.
+ *   - Every call is stream-ordered and asynchronous on `stream` (a hipStream_t;
+ *     NULL = default stream); nothing synchronises the host except
+ *     admm_ctx_create / admm_ctx_destroy / admm_batch_bind.
+ *   - Return 0 on success; a negative code on failure, with a message
+ *     available from admm_last_error() (thread-local).
+ *   - One context per device, used from one host thread.
+ */
+#ifndef ADMM_TOMO_H
+#define ADMM_TOMO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ADMM_ABI_VERSION 1
+
+#define ADMM_OK 0
+#define ADMM_E_INVALID (-1)
+#define ADMM_E_HIP (-2)
+#define ADMM_E_STATE (-3)
+
+#define ADMM_DTYPE_F32 0
+#define ADMM_DTYPE_F64 1
+
+#define ADMM_TV_ISO 0
+#define ADMM_TV_ANISO 1
+
+/* per-node statistics written by admm_node_update (float64) */
+#define ADMM_NODE_STAT_MSE_SINO 0 /* ||A x - b||^2           (block_6_admm_loop_ver2.py:190-194) */
+#define ADMM_NODE_STAT_G2 1       /* ||g||^2 stationarity    (block_6_admm_loop_ver2.py:145-149) */
+#define ADMM_NODE_STAT_TV 2       /* TV(x)                   (block_4_tv_helpers.py:5-14) */
+#define ADMM_NODE_STAT_QUAD 3     /* sum_j rho/2 ||x-v_ij||^2_Q (block_5_node_problem.py:26-29) */
+#define ADMM_NODE_STAT_IMG 4      /* ||x - phantom||^2       (block_6_admm_loop_ver2.py:199-204) */
+#define ADMM_NODE_STATS 5
+
+/* per-edge statistics written by admm_consensus (float64) */
+#define ADMM_EDGE_STAT_RA2 0 /* ||x_a - z||^2 */
+#define ADMM_EDGE_STAT_RB2 1 /* ||x_b - z||^2 */
+#define ADMM_EDGE_STAT_DZ2 2 /* ||z_new - z_old||^2 */
+#define ADMM_EDGE_STATS 3
+
+/* Parallel-beam geometry of one graph node.  Replaces the ODL construction of
+ * block_2_load_odl_data.py:34-83: space [-1,1]^2 (N x N), angles
+ * uniform_partition(angle_min, angle_max, n_angles) midpoints, detector
+ * uniform_partition(det_min, det_max, n_det) midpoints.  All nodes share it. */
+typedef struct admm_geom {
+    int32_t N;
+    int32_t n_angles;
+    int32_t n_det;
+    int32_t reserved;
+    double angle_min, angle_max;
+    double det_min, det_max;
+} admm_geom;
+
+typedef struct admm_ctx admm_ctx;
+
+/* The batch of graph nodes this device updates, their incident edges and the
+ * solver parameters.  All pointers are device pointers. */
+typedef struct admm_batch {
+    int32_t V;        /* local graph nodes (rows 0..V-1 of x_ext) */
+    int32_t n_xext;   /* rows of x_ext: local nodes + halo (neighbour) nodes */
+    int32_t n_edges;  /* edge slots stored on this device */
+    int32_t tv_iters; /* split-Bregman rounds per x-update (T_tv) */
+    int32_t cg_iters; /* CG steps per round (K_cg) */
+    int32_t tv_kind;  /* ADMM_TV_ISO / ADMM_TV_ANISO */
+    double rho, lam, mu;
+
+    double* x_ext;        /* [n_xext][n]  node images; rows < V updated in place   */
+    double* d;            /* [V][2][n]    split variable d ~ Kx (warm state)        */
+    double* e;            /* [V][2][n]    Bregman variable (warm state)             */
+    const double* atb;    /* [V][n]       A^T b                                     */
+    const double* dsum;   /* [V][n]       D_i = sum_j q_ij                          */
+    const void* b;        /* [V][m]       sinograms (context dtype)                 */
+    const double* phantom;/* [n] or NULL  for ||x - phantom||^2                     */
+
+    double* y;            /* [E][n] dual of the lower-numbered endpoint (y_ij,min)  */
+    double* z;            /* [E][n] consensus z_ij                                  */
+    const double* q;      /* [Qslots][n] precision vectors                         */
+    const int32_t* edge_a;    /* [E] x_ext row of the lower endpoint               */
+    const int32_t* edge_b;    /* [E] x_ext row of the higher endpoint              */
+    const int32_t* inc_off;   /* [V+1] CSR over local nodes of incident edge-ends  */
+    const int32_t* inc_edge;  /* [nnz] edge slot                                   */
+    const int32_t* inc_qslot; /* [nnz] q slot of q_ij seen from this node           */
+    const int32_t* inc_sign;  /* [nnz] +1 if this node is the lower endpoint, else -1 */
+
+    double* node_stats;   /* [V][ADMM_NODE_STATS] */
+    double* edge_stats;   /* [E][ADMM_EDGE_STATS] */
+} admm_batch;
+
+int admm_abi_version(void);
+const char* admm_last_error(void);
+
+/* Context: geometry tables + scratch.  dtype = ADMM_DTYPE_*.  max_images bounds
+ * the batch size of the operator entry points below. */
+int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_images, int device);
+int admm_ctx_destroy(admm_ctx* ctx);
+
+/* --- operator entry points (replace ODL RayTransform / dense A) ---------- */
+
+/* sino[v] = A img[v] for v < nimg.  Replaces `Ai @ x`
+ * (block_5_node_problem.py:21, block_6_admm_loop_ver2.py:193). */
+int admm_project_fwd(admm_ctx* ctx, const void* img, void* sino, int nimg, void* stream);
+/* img[v] = A^T sino[v].  Replaces `Ai.T @ r` (block_6_admm_loop_ver2.py:145). */
+int admm_project_adj(admm_ctx* ctx, const void* sino, void* img, int nimg, void* stream);
+/* W[p] = max(sum_r A[r,p]^2, 1e-12) (float64).  Replaces make_precisions'
+ * column sums (block_3_graph_and_precisions.py:20-23, block_1_env_and_imports.py:16-18). */
+int admm_column_norms_sq(admm_ctx* ctx, double* W, void* stream);
+/* (gx, gy) = K x, forward differences (block_4_tv_helpers.py:17-23), float64. */
+int admm_tv_grad(admm_ctx* ctx, const double* x, double* gx, double* gy, int nimg, void* stream);
+/* out = K^T (px, py), exact adjoint of admm_tv_grad (block_4_tv_helpers.py:25-35). */
+int admm_tv_div(admm_ctx* ctx, const double* px, const double* py, double* out, int nimg,
+                void* stream);
+
+/* --- node batch (replaces the node loop + CVXPY/SCS solve and the edge updates) --- */
+
+/* Bind a batch (pointers are captured; the contents may change between calls).
+ * Allocates scratch and records the update sequence as a hipGraph.  Synchronous. */
+int admm_batch_bind(admm_ctx* ctx, const admm_batch* batch);
+/* A^T b for the bound batch (setup; writes batch->atb, which is then const). */
+int admm_batch_atb(admm_ctx* ctx, double* atb_out, void* stream);
+/* One x-update of every bound node: neighbour gather v_ij = z_ij - y_ij,i,
+ * fixed-count split-Bregman/CG solve of eq.(1), diagnostics into node_stats.
+ * Replaces block_6_admm_loop_ver2.py:81-197 (build_node_problem + SCS + g check). */
+int admm_node_update(admm_ctx* ctx, void* stream);
+/* Edge updates z = (a_i + a_j)/2, y += x - z and the residual partial sums
+ * into edge_stats.  Replaces block_6_admm_loop_ver2.py:210-253.  Every edge
+ * slot of the batch is processed; x_ext halo rows must be current. */
+int admm_consensus(admm_ctx* ctx, void* stream);
+/* Average duration (ms) of `reps` back-to-back launches of the forward
+ * projector on the bound batch's current x, timed with HIP events on `stream`.
+ * Measurement helper for bench.py; synchronises. */
+int admm_time_forward(admm_ctx* ctx, int reps, void* stream, double* ms_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ADMM_TOMO_H */

@@ -1,0 +1,155 @@
+"""Oracle: decentralized edge-split ADMM loop.  TEST INFRASTRUCTURE ONLY.
+
+Restates /root/reference/block_6_admm_loop_ver2.py:15-326 with the node solve
+of ``node_solver`` (fixed-count split-Bregman + CG instead of CVXPY+SCS):
+
+  * state init x=0, z=0, y=0 (:35-43); b_i = sinograms[i].reshape(-1) (:46)
+  * neighbour gather v_ij = z_ij - y_ij,i, q_ij = Qij_diag_fn(i,j) (:85-95)
+  * eps_target = 2/(k+1)^1.005, first SCS eps = min(1e-2, eps_target) (:101-108)
+  * z_ij = (a_i + a_j)/2 with a = x + y (:210-223); y += x - z (:225-230)
+  * r2, s2, per-node attribution, sqrt, stop test (:232-289)
+  * history keys (:310-326)
+
+Edge state is kept in the single-y form the device uses: y_e is the dual of
+the lower-numbered endpoint a, the other endpoint's dual is -y_e (with y0=0,
+y_ij,i + y_ij,j = 0 holds after every update -- SURVEY.md 8a row a7).  Both
+ends then evaluate  a_a = x_a + y_e,  a_b = x_b - y_e,  z = (a_a + a_b)/2,
+y_e += x_a - z  in that order.  ``edge_update_literal`` restates the
+reference's two-dual dict form verbatim for cross-checking.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from . import node_solver as ns
+
+HISTORY_KEYS = (
+    "primal", "dual", "pri_per_node", "dual_per_node", "obj_per_node", "obj_total",
+    "mse_sino_per_node", "mse_sino_total", "img_mse_per_node", "img_mse_total",
+    "g_norm_history", "eps_used_history", "eps_target_history",
+)
+
+
+def canonical_edges(G) -> list[tuple[int, int]]:
+    """Edges as (min, max) in ``G.edges()`` order (block_6_admm_loop_ver2.py:39-40)."""
+    return [(min(i, j), max(i, j)) for i, j in G.edges()]
+
+
+def eps_target(k: int) -> float:
+    return 2.0 / ((k + 1) ** 1.005)  # block_6_admm_loop_ver2.py:101-103
+
+
+def edge_update_literal(G, x, y, z):
+    """Verbatim restatement of block_6_admm_loop_ver2.py:210-230 (two duals per edge)."""
+    new_z = {}
+    for i, j in G.edges():
+        key = (min(i, j), max(i, j))
+        a_i = x[i] + y[(key[0], key[1], i)]
+        a_j = x[j] + y[(key[0], key[1], j)]
+        new_z[key] = (a_i + a_j) / 2.0
+    new_y = {}
+    for i, j in G.edges():
+        key = (min(i, j), max(i, j))
+        new_y[(key[0], key[1], i)] = y[(key[0], key[1], i)] + x[i] - new_z[key]
+        new_y[(key[0], key[1], j)] = y[(key[0], key[1], j)] + x[j] - new_z[key]
+    return new_z, new_y
+
+
+def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
+                       max_iters=10, eps_pri=1e-1, eps_dual=1e-1, phantom_true=None,
+                       mu=None, tv_iters=10, cg_iters=5, tv_kind="iso",
+                       dtype=np.float64, node_subset=None):
+    """Oracle ADMM.  ``ops`` = list of scipy sparse matrices (one per node).
+
+    Returns (x_list, history) with the reference's history keys.  With
+    ``node_subset`` only those nodes' x-updates run (the others keep x=0); used
+    only to time a bounded CPU sample.
+    """
+    V = len(ops)
+    n = N * N
+    mu = (10.0 * lam_tv if mu is None else mu)
+    prm = ns.NodeParams(rho=rho, lam=lam_tv, mu=mu, tv_iters=tv_iters, cg_iters=cg_iters,
+                        tv_kind=tv_kind)
+    edges = canonical_edges(G)
+    b = [np.asarray(s, dtype=np.float64).reshape(-1) for s in sinograms]
+    ATs = [A.T.tocsr() for A in ops]
+    Atb = [ATs[i] @ b[i] for i in range(V)]
+    states = [ns.NodeState.zeros(n, dtype) for _ in range(V)]
+    y = {e: np.zeros(n) for e in edges}
+    z = {e: np.zeros(n) for e in edges}
+    nbrs = {i: list(G.neighbors(i)) for i in range(V)}
+    hist = {k: [] for k in HISTORY_KEYS}
+    ph = None
+    if phantom_true is not None:
+        ph = np.asarray(phantom_true, dtype=np.float64).reshape(-1)
+    x = [np.zeros(n) for _ in range(V)]
+    for k in range(max_iters):
+        obj_i = np.zeros(V)
+        g_i = np.zeros(V)
+        mse_i = np.zeros(V)
+        et = eps_target(k)
+        todo = range(V) if node_subset is None else node_subset
+        for i in todo:
+            qv = []
+            D = np.zeros(n)
+            c = np.zeros(n)
+            for j in nbrs[i]:
+                e = (min(i, j), max(i, j))
+                yi = y[e] if i == e[0] else -y[e]
+                v = z[e] - yi
+                q = np.asarray(Qij_diag_fn(i, j), dtype=np.float64)
+                D += q
+                c += q * v
+                qv.append((q, v))
+            d = ns.node_update(ops[i], Atb[i], b[i], D, c, qv, states[i], N, prm, dtype=dtype,
+                               AT=ATs[i])
+            obj_i[i] = d.obj
+            g_i[i] = d.g_norm
+            mse_i[i] = d.mse_sino
+        x = [st.x.astype(np.float64) for st in states]
+        hist["g_norm_history"].append(g_i)
+        hist["eps_used_history"].append(np.full(V, min(1e-2, et)))
+        hist["eps_target_history"].append(np.full(V, et))
+        hist["mse_sino_per_node"].append(mse_i)
+        hist["mse_sino_total"].append(float(np.sum(mse_i)))
+        if ph is not None:
+            img = np.array([float((xi - ph) @ (xi - ph)) for xi in x])
+        else:
+            img = np.full(V, np.nan)
+        hist["img_mse_per_node"].append(img)
+        hist["img_mse_total"].append(float(np.sum(img)))
+        r2 = 0.0
+        s2 = 0.0
+        pri = np.zeros(V)
+        dua = np.zeros(V)
+        for (a_, b_) in edges:
+            e = (a_, b_)
+            aa = x[a_] + y[e]
+            ab = x[b_] - y[e]
+            zn = (aa + ab) * 0.5
+            y[e] = y[e] + x[a_] - zn
+            ra = x[a_] - zn
+            rb = x[b_] - zn
+            dz = zn - z[e]
+            z[e] = zn
+            ra2 = float(ra @ ra)
+            rb2 = float(rb @ rb)
+            dz2 = float(dz @ dz)
+            r2 += ra2 + rb2
+            pri[a_] += ra2
+            pri[b_] += rb2
+            s2 += rho * rho * dz2
+            dua[a_] += rho * rho * dz2
+            dua[b_] += rho * rho * dz2
+        pn, dn = math.sqrt(r2), math.sqrt(s2)
+        hist["primal"].append(pn)
+        hist["dual"].append(dn)
+        hist["obj_per_node"].append(obj_i)
+        hist["obj_total"].append(float(np.sum(obj_i)))
+        hist["pri_per_node"].append(np.sqrt(pri))
+        hist["dual_per_node"].append(np.sqrt(dua))
+        if pn < eps_pri and dn < eps_dual:
+            break
+    return x, hist

@@ -1,0 +1,141 @@
+"""GPU parity of the full decentralized ADMM hot path vs the CPU oracle.
+
+Same inputs on both sides (the GPU-synthesised float32 sinograms, cast to
+float64 for the oracle).  North-star tolerance: reconstructed images and the
+primal / dual residual trajectories within 1e-5 relative Frobenius of the
+float64 oracle (float32 projector samples, float64 solver state).  With float64
+samples (the C5 configuration) the bar is 1e-9.
+"""
+import networkx as nx
+import numpy as np
+import pytest
+import torch
+
+from admm_hip.data import make_precisions, make_sinograms, shepp_logan
+from admm_hip.solver import make_operators
+from block_5_node_problem import build_node_problem
+from block_6_admm_loop_ver2 import decentralized_admm
+import block_6_admm_loop
+from oracle import admm as oadmm
+from oracle import node_solver as ons
+from oracle.geometry import Geometry, joseph_matrix
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def setup_problem(N, V, angles_total, dtype="float32", seed=1000):
+    ops = make_operators(N, V, angles_total, dtype=dtype, device=0)
+    ph = shepp_logan(N)
+    sinos = make_sinograms(ops, ph, 0.005, seed=seed)
+    Wi, Q = make_precisions(ops)
+    A = joseph_matrix(Geometry(N, ops[0].geom.n_angles))
+    sin_h = [s.double().cpu().numpy() for s in sinos]
+    return ops, ph.numpy(), sinos, Wi, Q, A, sin_h
+
+
+def compare(G, N, V, iters, angles_total, dtype="float32", tol=1e-5, tv_kind="iso", lam=0.02,
+            rho=2.0, tv_iters=10, cg_iters=5):
+    ops, ph, sinos, Wi, Q, A, sin_h = setup_problem(N, V, angles_total, dtype)
+    x, h = decentralized_admm(ops, sinos, G, Wi, Q, N, lam_tv=lam, rho=rho, max_iters=iters,
+                              eps_pri=0.0, eps_dual=0.0, verbose=False, phantom_true=ph,
+                              tv_kind=tv_kind, tv_iters=tv_iters, cg_iters=cg_iters,
+                              write_params=False)
+    xo, ho = oadmm.decentralized_admm([A] * V, sin_h, G, Q, N, lam_tv=lam, rho=rho,
+                                      max_iters=iters, eps_pri=0.0, eps_dual=0.0, phantom_true=ph,
+                                      tv_kind=tv_kind, tv_iters=tv_iters, cg_iters=cg_iters)
+    assert set(h) >= set(oadmm.HISTORY_KEYS)
+    errs = {"x": rel(np.stack(x), np.stack(xo))}
+    for k in ("primal", "dual"):
+        errs[k] = rel(h[k], ho[k])
+    for k in ("obj_total", "mse_sino_total", "img_mse_total"):
+        errs[k] = rel(h[k], ho[k])
+    errs["g"] = rel(np.stack(h["g_norm_history"]), np.stack(ho["g_norm_history"]))
+    print({k: f"{v:.2e}" for k, v in errs.items()})
+    assert errs["x"] < tol and errs["primal"] < tol and errs["dual"] < tol, errs
+    # diagnostics: same formulas; tolerance covers the float32 A x - b cancellation
+    for k in ("obj_total", "mse_sino_total", "img_mse_total", "g"):
+        assert errs[k] < max(10 * tol, 1e-4), (k, errs)
+    return x, h, xo, ho
+
+
+def test_c1_ring_64_matches_oracle(cuda):
+    """BASELINE configs[0]: 64^2 Shepp-Logan, 4-node ring, 20 ADMM iterations."""
+    compare(nx.cycle_graph(4), 64, 4, 20, None)
+
+
+def test_erdos_renyi_matches_oracle(cuda):
+    G = nx.erdos_renyi_graph(6, 0.6, seed=3)
+    assert nx.is_connected(G)
+    compare(G, 32, 6, 8, 96)
+
+
+def test_complete_graph_anisotropic_matches_oracle(cuda):
+    compare(nx.complete_graph(5), 32, 5, 6, 100, tv_kind="aniso")
+
+
+def test_float64_samples_tight(cuda):
+    """C5 arithmetic (float64 samples): agreement to 1e-9."""
+    compare(nx.cycle_graph(3), 32, 3, 6, 96, dtype="float64", tol=1e-9)
+
+
+def test_odd_tv_rounds_and_single_cg(cuda):
+    compare(nx.path_graph(3), 24, 3, 4, 72, tv_iters=3, cg_iters=1)
+
+
+def test_deterministic_bitwise(cuda):
+    ops, ph, sinos, Wi, Q, A, _ = setup_problem(48, 4, 96)
+    G = nx.cycle_graph(4)
+    runs = [decentralized_admm(ops, sinos, G, Wi, Q, 48, lam_tv=0.02, rho=2.0, max_iters=3,
+                               verbose=False, write_params=False) for _ in range(2)]
+    assert all(np.array_equal(a, b) for a, b in zip(runs[0][0], runs[1][0]))
+    assert runs[0][1]["primal"] == runs[1][1]["primal"]
+
+
+def test_stop_criterion_and_ver1_surface(cuda):
+    ops, ph, sinos, Wi, Q, A, _ = setup_problem(32, 3, 96)
+    x, h = block_6_admm_loop.decentralized_admm(ops, sinos, nx.cycle_graph(3), Wi, Q, 32,
+                                                lam_tv=0.02, rho=2.0, max_iters=50,
+                                                eps_pri=1e9, eps_dual=1e9, verbose=False,
+                                                scs_total_iters=7, scs_chunk_iters=3,
+                                                write_params=False)
+    assert len(h["primal"]) == 1  # stopped after the first iteration (_ver2:286-289)
+    assert h["primal_res"] is h["primal"] and h["obj"] is h["obj_total"]
+
+
+def test_build_node_problem_matches_oracle(cuda):
+    """block_5 surface: one node with two neighbour terms, two warm-started solves."""
+    N = 40
+    ops, ph, sinos, Wi, Q, A, sin_h = setup_problem(N, 1, 60)
+    rng = np.random.default_rng(5)
+    vs = [ph.ravel() + 0.05 * rng.standard_normal(N * N) for _ in range(2)]
+    qs = [Wi[0] * (1.0 + 0.5 * rng.random(N * N)) for _ in range(2)]
+    xi, prob = build_node_problem(ops[0], sinos[0].reshape(-1), 2.0, vs, N, 0.02, qs)
+    st = ons.NodeState.zeros(N * N)
+    b = sin_h[0].reshape(-1)
+    D = qs[0] + qs[1]
+    c = qs[0] * vs[0] + qs[1] * vs[1]
+    prm = ons.NodeParams(rho=2.0, lam=0.02, mu=0.2)
+    for _ in range(2):
+        prob.solve(solver="SCS", eps=1e-2, max_iters=50, warm_start=True, verbose=False,
+                   acceleration_lookback=20)
+        d = ons.node_update(A, A.T @ b, b, D, c, list(zip(qs, vs)), st, N, prm)
+        assert rel(xi.value, st.x) < 1e-5
+        assert abs(prob.value - d.obj) / abs(d.obj) < 1e-5
+    assert prob.solver_stats.num_iters == 50 and prob.status == "optimal_inaccurate"
+
+
+def test_build_node_problem_no_neighbours_no_tv(cuda):
+    """test_block5_with_aggregate.py:59-67 shape: rho=0, no neighbours; lam=0 -> least squares."""
+    N = 24
+    ops, ph, sinos, Wi, Q, A, sin_h = setup_problem(N, 1, 72)
+    xi, prob = build_node_problem(ops[0], sinos[0].reshape(-1), 0.0, [], N, 0.0, [])
+    prob.solve(max_iters=200)
+    b = sin_h[0].reshape(-1)
+    r0 = np.linalg.norm(b)
+    r1 = np.linalg.norm(A @ xi.value - b)
+    assert r1 < 0.1 * r0

@@ -1,0 +1,85 @@
+"""GPU: size-independent properties at the BASELINE workload size (512^2, 96 angles,
+8 nodes on one GPU, ring) -- the oracle is too slow to replay it here.
+
+* every ADMM iteration decreases nothing it should not: the stored edge state
+  satisfies z = (x_a + x_b)/2 (single-y invariant);
+* the x-update is a descent step on eq.(1) from x = 0;
+* two runs are bitwise identical (fixed-order reductions, no atomics);
+* one node-update of one node agrees with the oracle (single node, 512^2).
+"""
+import networkx as nx
+import numpy as np
+import pytest
+import torch
+
+from admm_hip.data import make_precisions, make_sinograms, shepp_logan
+from admm_hip.exchange import HaloExchange
+from admm_hip.plan import make_plan
+from admm_hip.solver import NodeBatch, make_operators
+
+pytestmark = pytest.mark.gpu
+
+N, V, A_PER = 512, 8, 96
+
+
+@pytest.fixture(scope="module")
+def problem(cuda):
+    ops = make_operators(N, V, angles_total=A_PER * V, device=0)
+    ph = shepp_logan(N)
+    sinos = make_sinograms(ops, ph, 0.005)
+    Wi, Q = make_precisions(ops)
+    return ops, ph, sinos, Wi, Q
+
+
+def run(problem, iters):
+    ops, ph, sinos, Wi, Q = problem
+    G = nx.cycle_graph(V)
+    plan = make_plan(G, V)
+    nb = NodeBatch(ops[0].geom, "float32", plan, sinos, Q, 2.0, 0.02, 0.2, 10, 5, "iso", ph, 0)
+    stats = []
+    for _ in range(iters):
+        nb.node_update()
+        nb.consensus()
+        stats.append(nb.node_stats.cpu().numpy().copy())
+    torch.cuda.synchronize()
+    return nb, plan, stats
+
+
+def test_fullsize_invariants_and_descent(problem):
+    nb, plan, stats = run(problem, 2)
+    x = nb.x_ext
+    for k, (a, b) in enumerate(plan.edges):
+        z = nb.z[k]
+        assert torch.allclose(z, 0.5 * (x[a] + x[b]), rtol=0, atol=1e-12 * float(x.abs().max()))
+    ops, ph, sinos, Wi, Q = problem
+    # objective at x=0 is 0.5||b||^2 (neighbour terms vanish at z=y=0) -> first update descends
+    b2 = torch.stack([s.double().reshape(-1) for s in sinos]).pow(2).sum(dim=1).cpu().numpy()
+    obj1 = 0.5 * stats[0][:, 0] + 0.02 * stats[0][:, 2] + stats[0][:, 3]
+    assert np.all(obj1 < 0.5 * b2)
+    assert np.all(np.isfinite(stats[1]))
+
+
+def test_fullsize_bitwise_repeatable(problem):
+    nb1, _, s1 = run(problem, 1)
+    nb2, _, s2 = run(problem, 1)
+    assert torch.equal(nb1.x_ext, nb2.x_ext)
+    assert np.array_equal(s1[0], s2[0])
+
+
+def test_fullsize_single_node_update_vs_oracle(problem):
+    from oracle import node_solver as ons
+    from oracle.geometry import Geometry, joseph_matrix
+    ops, ph, sinos, Wi, Q = problem
+    G = nx.path_graph(2)
+    plan = make_plan(G, 2)
+    nb = NodeBatch(ops[0].geom, "float32", plan, sinos, Q, 2.0, 0.02, 0.2, 2, 3, "iso", None, 0)
+    nb.node_update()
+    torch.cuda.synchronize()
+    A = joseph_matrix(Geometry(N, A_PER))
+    b = sinos[0].double().cpu().numpy().reshape(-1)
+    q = Q(0, 1)
+    st = ons.NodeState.zeros(N * N)
+    ons.node_update(A, A.T @ b, b, q, np.zeros(N * N), [(q, np.zeros(N * N))], st, N,
+                    ons.NodeParams(rho=2.0, lam=0.02, mu=0.2, tv_iters=2, cg_iters=3))
+    x = nb.x_ext[0].cpu().numpy()
+    assert np.linalg.norm(x - st.x) / np.linalg.norm(st.x) < 1e-5
