@@ -11,6 +11,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "../../include/admm_tomo.h"
@@ -72,7 +74,8 @@ struct admm_ctx {
   // batch
   bool bound = false;
   admm_batch b{};
-  Buf xs, xsT, p, pT, Hp, sino, r, c, d2, e2;
+  int vb = 1;  // node interleave width of the sample buffers
+  Buf xs, xsT, p, pT, Hp, sino, bI, r, c, d2, e2;
   Buf partH, partRR, partS, partD, partE;
   Buf redH, rrslot;
   int P_back = 0, P_tile = 0, P_fwd = 0, P_edge = 0;
@@ -85,52 +88,42 @@ namespace {
 
 int vb_for(int V) { return V >= 5 ? 8 : (V >= 3 ? 4 : (V == 2 ? 2 : 1)); }
 
-template <typename T, int VB, int MODE>
-void launch_fwd_vb(admm_ctx* C, const T* img, const T* imgT, T* sino, const T* b, double* part, int V,
-                   hipStream_t s) {
-  dim3 grid((C->g.n_det + kFwdRays - 1) / kFwdRays, C->g.n_angles, (V + VB - 1) / VB);
-  hipLaunchKernelGGL((k_fwd<T, VB, MODE>), grid, dim3(kBlock), 0, s, img, imgT, sino, b, part, C->fang,
-                     C->g.N, C->g.n_det, C->g.n_angles, V);
+template <typename F>
+int with_vb(int vb, F&& f) {
+  switch (vb) {
+    case 8: return f(std::integral_constant<int, 8>{});
+    case 4: return f(std::integral_constant<int, 4>{});
+    case 2: return f(std::integral_constant<int, 2>{});
+    default: return f(std::integral_constant<int, 1>{});
+  }
 }
 
-template <typename T, int MODE>
-int launch_fwd(admm_ctx* C, const T* img, const T* imgT, T* sino, const T* b, double* part, int V,
-               hipStream_t s) {
-  switch (vb_for(V)) {
-    case 8: launch_fwd_vb<T, 8, MODE>(C, img, imgT, sino, b, part, V, s); break;
-    case 4: launch_fwd_vb<T, 4, MODE>(C, img, imgT, sino, b, part, V, s); break;
-    case 2: launch_fwd_vb<T, 2, MODE>(C, img, imgT, sino, b, part, V, s); break;
-    default: launch_fwd_vb<T, 1, MODE>(C, img, imgT, sino, b, part, V, s); break;
-  }
+#define RET(expr)                   \
+  do {                              \
+    int _rc = (expr);               \
+    if (_rc != ADMM_OK) return _rc; \
+  } while (0)
+
+template <typename T, int VB, int MODE>
+int launch_fwd(admm_ctx* C, const T* img, const T* imgT, T* sino, const T* b, double* part, int V, hipStream_t s) {
+  dim3 grid((C->g.n_det + kFwdRays - 1) / kFwdRays, C->g.n_angles, (V + VB - 1) / VB);
+  hipLaunchKernelGGL((k_fwd<T, VB, MODE>), grid, dim3(kBlock), 0, s, img, imgT, sino, b, part, C->fang, C->g.N,
+                     C->g.n_det, C->g.n_angles, V);
   CHECK_LAUNCH();
   return ADMM_OK;
 }
 
 template <typename T, int VB, int MODE>
-void launch_back_vb(admm_ctx* C, const BackArgs<T>& a, int V, hipStream_t s) {
-  const int N = C->g.N;
-  dim3 grid((N + kBackTileJ - 1) / kBackTileJ, (N + kBackTileI - 1) / kBackTileI,
-            MODE == BACK_WSQ ? 1 : (V + VB - 1) / VB);
-  hipLaunchKernelGGL((k_back<T, VB, MODE>), grid, dim3(kBlock), 0, s, a);
-}
-
-template <typename T, int MODE>
 int launch_back(admm_ctx* C, BackArgs<T> a, int V, hipStream_t s) {
   a.ang = C->bang;
   a.N = C->g.N;
   a.n_det = C->g.n_det;
   a.n_ang = C->g.n_angles;
   a.V = V;
-  if (MODE == BACK_WSQ) {
-    launch_back_vb<T, 1, MODE>(C, a, 1, s);
-  } else {
-    switch (vb_for(V)) {
-      case 8: launch_back_vb<T, 8, MODE>(C, a, V, s); break;
-      case 4: launch_back_vb<T, 4, MODE>(C, a, V, s); break;
-      case 2: launch_back_vb<T, 2, MODE>(C, a, V, s); break;
-      default: launch_back_vb<T, 1, MODE>(C, a, V, s); break;
-    }
-  }
+  const int N = C->g.N;
+  dim3 grid((N + kBackTileJ - 1) / kBackTileJ, (N + kBackTileI - 1) / kBackTileI,
+            MODE == BACK_WSQ ? 1 : (V + VB - 1) / VB);
+  hipLaunchKernelGGL((k_back<T, VB, MODE>), grid, dim3(kBlock), 0, s, a);
   CHECK_LAUNCH();
   return ADMM_OK;
 }
@@ -139,9 +132,9 @@ int back_partitions(admm_ctx* C) {
   const int N = C->g.N;
   return ((N + kBackTileJ - 1) / kBackTileJ) * ((N + kBackTileI - 1) / kBackTileI);
 }
-dim3 tile_grid(admm_ctx* C, int V) {
+dim3 tile_grid(admm_ctx* C, int nchunks) {
   const int N = C->g.N;
-  return dim3((N + kTile - 1) / kTile, (N + kTile - 1) / kTile, V);
+  return dim3((N + kTile - 1) / kTile, (N + kTile - 1) / kTile, nchunks);
 }
 
 int launch_reduce(const double* part, int rows, int P, double* out, int G, int ostride, int ooff, hipStream_t s) {
@@ -150,20 +143,15 @@ int launch_reduce(const double* part, int rows, int P, double* out, int G, int o
   return ADMM_OK;
 }
 
-#define RET(expr)                 \
-  do {                            \
-    int _rc = (expr);             \
-    if (_rc != ADMM_OK) return _rc; \
-  } while (0)
-
 // --------------------------------------------------------------------------
 // the x-update sequence for the bound batch (replaces block_6_admm_loop_ver2.py:81-197)
 // --------------------------------------------------------------------------
-template <typename T>
+template <typename T, int VB>
 int enqueue_update(admm_ctx* C, hipStream_t s) {
   const admm_batch& B = C->b;
   const int V = B.V, N = C->g.N;
   const size_t npix = (size_t)N * N;
+  const int nch = (V + VB - 1) / VB;
   T* xs = (T*)C->xs.p;
   T* xsT = (T*)C->xsT.p;
   T* p = (T*)C->p.p;
@@ -174,15 +162,15 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
   double* c = (double*)C->c.p;
   double* redH = (double*)C->redH.p;
   double* rrslot = (double*)C->rrslot.p;
-  const dim3 tg = tile_grid(C, V);
+  const dim3 tg = tile_grid(C, nch);
   const int Pt = C->P_tile, Pb = C->P_back;
 
-  // 1. neighbour gather: c = sum_j q_ij (z_ij - y_ij,i); xs = (T) x
-  hipLaunchKernelGGL(k_gather<T>, tg, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.q, B.inc_off, B.inc_edge,
-                     B.inc_qslot, B.inc_sign, c, xs, xsT, N);
+  // 1. neighbour gather: c = sum_j q_ij (z_ij - y_ij,i); xs = (T) x (+ transpose)
+  hipLaunchKernelGGL((k_gather<T, VB>), tg, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.q, B.inc_off, B.inc_edge,
+                     B.inc_qslot, B.inc_sign, c, xs, xsT, N, V);
   CHECK_LAUNCH();
   // 2-4. r = A^T b + rho c + mu K^T(d - e) - H x,  p = r,  rr
-  RET((launch_fwd<T, 0>(C, xs, xsT, sino, nullptr, nullptr, V, s)));
+  RET((launch_fwd<T, VB, 0>(C, xs, xsT, sino, nullptr, nullptr, V, s)));
   {
     BackArgs<T> a{};
     a.sino = sino;
@@ -198,10 +186,10 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
     a.rho = B.rho;
     a.lam = B.lam;
     a.mu = B.mu;
-    RET((launch_back<T, BACK_INIT>(C, a, V, s)));
+    RET((launch_back<T, VB, BACK_INIT>(C, a, V, s)));
   }
   RET(launch_reduce((double*)C->partRR.p, V, Pb, rrslot, 1, 1, 0, s));
-  hipLaunchKernelGGL(k_transpose<T>, tg, dim3(kBlock), 0, s, p, pT, N);
+  hipLaunchKernelGGL((k_transpose<T, VB>), tg, dim3(kBlock), 0, s, p, pT, N);
   CHECK_LAUNCH();
 
   const double tau = B.lam / B.mu;
@@ -213,7 +201,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
   for (int t = 0; t < Tt; ++t) {
     for (int kk = 0; kk < K; ++kk) {
       const int it = t * K + kk;
-      RET((launch_fwd<T, 0>(C, p, pT, sino, nullptr, nullptr, V, s)));
+      RET((launch_fwd<T, VB, 0>(C, p, pT, sino, nullptr, nullptr, V, s)));
       BackArgs<T> a{};
       a.sino = sino;
       a.out_t = Hp;
@@ -224,21 +212,21 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
       a.rho = B.rho;
       a.lam = B.lam;
       a.mu = B.mu;
-      RET((launch_back<T, BACK_H>(C, a, V, s)));
+      RET((launch_back<T, VB, BACK_H>(C, a, V, s)));
       RET(launch_reduce((double*)C->partH.p, 3 * V, Pb, redH, 1, 1, 0, s));
-      hipLaunchKernelGGL(k_cg_update<T>, tg, dim3(kBlock), 0, s, B.x_ext, r, p, pT, Hp, redH,
-                         rrslot + (size_t)it * V, rrslot + (size_t)(it + 1) * V, N);
+      hipLaunchKernelGGL((k_cg_update<T, VB>), tg, dim3(kBlock), 0, s, B.x_ext, r, p, pT, Hp, redH,
+                         rrslot + (size_t)it * V, rrslot + (size_t)(it + 1) * V, N, V);
       CHECK_LAUNCH();
     }
     const bool last = (t + 1 == Tt);
     if (!last) {
-      hipLaunchKernelGGL((k_tv_update<T, false>), tg, dim3(kBlock), 0, s, B.x_ext, dcur, ecur, dnxt, enxt, r, p,
-                         pT, (double*)C->partRR.p, tau, B.mu, B.tv_kind, N);
+      hipLaunchKernelGGL((k_tv_update<T, VB, false>), tg, dim3(kBlock), 0, s, B.x_ext, dcur, ecur, dnxt, enxt, r,
+                         p, pT, (double*)C->partRR.p, tau, B.mu, B.tv_kind, N, V);
       CHECK_LAUNCH();
       RET(launch_reduce((double*)C->partRR.p, V, Pt, rrslot + (size_t)(t + 1) * K * V, 1, 1, 0, s));
     } else {
-      hipLaunchKernelGGL((k_tv_update<T, true>), tg, dim3(kBlock), 0, s, B.x_ext, dcur, ecur, dnxt, enxt, r, xs,
-                         xsT, (double*)nullptr, tau, B.mu, B.tv_kind, N);
+      hipLaunchKernelGGL((k_tv_update<T, VB, true>), tg, dim3(kBlock), 0, s, B.x_ext, dcur, ecur, dnxt, enxt, r,
+                         xs, xsT, (double*)nullptr, tau, B.mu, B.tv_kind, N, V);
       CHECK_LAUNCH();
     }
     std::swap(dcur, dnxt);
@@ -249,7 +237,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
     HIPCHK(hipMemcpyAsync(B.e, ecur, 2 * V * npix * sizeof(double), hipMemcpyDeviceToDevice, s));
   }
   // diagnostics epilogue: s = A x - b, ||s||^2, g, TV, quad, image error
-  RET((launch_fwd<T, 1>(C, xs, xsT, sino, (const T*)B.b, (double*)C->partS.p, V, s)));
+  RET((launch_fwd<T, VB, 1>(C, xs, xsT, sino, (const T*)B.b, (double*)C->partS.p, V, s)));
   {
     BackArgs<T> a{};
     a.sino = sino;
@@ -269,11 +257,16 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
     a.lam = B.lam;
     a.mu = B.mu;
     a.tv_kind = B.tv_kind;
-    RET((launch_back<T, BACK_DIAG>(C, a, V, s)));
+    RET((launch_back<T, VB, BACK_DIAG>(C, a, V, s)));
   }
   RET(launch_reduce((double*)C->partS.p, V, C->P_fwd, B.node_stats, 1, ADMM_NODE_STATS, ADMM_NODE_STAT_MSE_SINO, s));
   RET(launch_reduce((double*)C->partD.p, 4 * V, Pb, B.node_stats, 4, ADMM_NODE_STATS, ADMM_NODE_STAT_G2, s));
   return ADMM_OK;
+}
+
+template <typename T>
+int enqueue_update_any(admm_ctx* C, hipStream_t s) {
+  return with_vb(C->vb, [&](auto vbc) { return enqueue_update<T, decltype(vbc)::value>(C, s); });
 }
 
 int enqueue_consensus(admm_ctx* C, hipStream_t s) {
@@ -365,13 +358,13 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
     fa[t].A0 = c0 + (g.det_min / h + 0.5 * hd / h + c0 * be) / al;
     fa[t].A1 = (hd / h) / al;
     fa[t].dl = -be / al;
-    fa[t].L = (float)(h / std::fabs(al));
+    fa[t].L = h / std::fabs(al);
     fa[t].caseA = caseA ? 1 : 0;
     ba[t].Bi = cs * h / hd;
     ba[t].Bj = sn * h / hd;
     ba[t].B0 = -c0 * (ba[t].Bi + ba[t].Bj) - g.det_min / hd - 0.5;
-    ba[t].slope = (float)((hd / h) / std::fabs(al));
-    ba[t].L = (float)(h / std::fabs(al));
+    ba[t].slope = (hd / h) / std::fabs(al);
+    ba[t].L = h / std::fabs(al);
   }
   hipError_t e1 = hipMalloc(&C->fang, fa.size() * sizeof(FwdAngle));
   hipError_t e2 = hipMalloc(&C->bang, ba.size() * sizeof(BackAngle));
@@ -391,7 +384,7 @@ int admm_ctx_destroy(admm_ctx* C) {
   (void)hipSetDevice(C->device);
   (void)hipDeviceSynchronize();
   free_graphs(C);
-  Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->r, &C->c,
+  Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->bI, &C->r, &C->c,
                  &C->d2, &C->e2, &C->partH, &C->partRR, &C->partS, &C->partD, &C->partE, &C->redH, &C->rrslot};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
@@ -409,17 +402,19 @@ int admm_project_fwd(admm_ctx* C, const void* img, void* sino, int nimg, void* s
   const size_t ds = dsize(C->dtype);
   RET(ensure(C->op_imgT, (size_t)nimg * C->npix * ds));
   const dim3 tg = tile_grid(C, nimg);
+  // operator API: node-major images = interleave width 1
   if (C->dtype == ADMM_DTYPE_F32) {
-    hipLaunchKernelGGL(k_transpose<float>, tg, dim3(kBlock), 0, s, (const float*)img, (float*)C->op_imgT.p, C->g.N);
+    hipLaunchKernelGGL((k_transpose<float, 1>), tg, dim3(kBlock), 0, s, (const float*)img, (float*)C->op_imgT.p,
+                       C->g.N);
     CHECK_LAUNCH();
-    return launch_fwd<float, 0>(C, (const float*)img, (const float*)C->op_imgT.p, (float*)sino, nullptr, nullptr,
-                                nimg, s);
+    return launch_fwd<float, 1, 0>(C, (const float*)img, (const float*)C->op_imgT.p, (float*)sino, nullptr, nullptr,
+                                   nimg, s);
   }
-  hipLaunchKernelGGL(k_transpose<double>, tg, dim3(kBlock), 0, s, (const double*)img, (double*)C->op_imgT.p,
+  hipLaunchKernelGGL((k_transpose<double, 1>), tg, dim3(kBlock), 0, s, (const double*)img, (double*)C->op_imgT.p,
                      C->g.N);
   CHECK_LAUNCH();
-  return launch_fwd<double, 0>(C, (const double*)img, (const double*)C->op_imgT.p, (double*)sino, nullptr, nullptr,
-                               nimg, s);
+  return launch_fwd<double, 1, 0>(C, (const double*)img, (const double*)C->op_imgT.p, (double*)sino, nullptr,
+                                  nullptr, nimg, s);
 }
 
 int admm_project_adj(admm_ctx* C, const void* sino, void* img, int nimg, void* stream) {
@@ -430,12 +425,12 @@ int admm_project_adj(admm_ctx* C, const void* sino, void* img, int nimg, void* s
     BackArgs<float> a{};
     a.sino = (const float*)sino;
     a.out_t = (float*)img;
-    return launch_back<float, BACK_PLAIN>(C, a, nimg, s);
+    return launch_back<float, 1, BACK_PLAIN>(C, a, nimg, s);
   }
   BackArgs<double> a{};
   a.sino = (const double*)sino;
   a.out_t = (double*)img;
-  return launch_back<double, BACK_PLAIN>(C, a, nimg, s);
+  return launch_back<double, 1, BACK_PLAIN>(C, a, nimg, s);
 }
 
 int admm_column_norms_sq(admm_ctx* C, double* W, void* stream) {
@@ -444,11 +439,11 @@ int admm_column_norms_sq(admm_ctx* C, double* W, void* stream) {
   if (C->dtype == ADMM_DTYPE_F32) {
     BackArgs<float> a{};
     a.out_d = W;
-    return launch_back<float, BACK_WSQ>(C, a, 1, s);
+    return launch_back<float, 1, BACK_WSQ>(C, a, 1, s);
   }
   BackArgs<double> a{};
   a.out_d = W;
-  return launch_back<double, BACK_WSQ>(C, a, 1, s);
+  return launch_back<double, 1, BACK_WSQ>(C, a, 1, s);
 }
 
 int admm_tv_grad(admm_ctx* C, const double* x, double* gx, double* gy, int nimg, void* stream) {
@@ -491,13 +486,16 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   RET(free_graphs(C));
   C->b = B;
   const int V = B.V;
+  C->vb = vb_for(V);
+  const size_t Vp = (size_t)((V + C->vb - 1) / C->vb) * C->vb;  // padded to whole chunks
   const size_t ds = dsize(C->dtype);
-  RET(ensure(C->xs, V * npix * ds));
-  RET(ensure(C->xsT, V * npix * ds));
-  RET(ensure(C->p, V * npix * ds));
-  RET(ensure(C->pT, V * npix * ds));
-  RET(ensure(C->Hp, V * npix * ds));
-  RET(ensure(C->sino, V * m * ds));
+  RET(ensure(C->xs, Vp * npix * ds));
+  RET(ensure(C->xsT, Vp * npix * ds));
+  RET(ensure(C->p, Vp * npix * ds));
+  RET(ensure(C->pT, Vp * npix * ds));
+  RET(ensure(C->Hp, Vp * npix * ds));
+  RET(ensure(C->sino, Vp * m * ds));
+  RET(ensure(C->bI, Vp * m * ds));
   RET(ensure(C->r, V * npix * 8));
   RET(ensure(C->c, V * npix * 8));
   RET(ensure(C->d2, 2 * V * npix * 8));
@@ -505,6 +503,8 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   C->P_back = back_partitions(C);
   const int N = C->g.N;
   C->P_tile = ((N + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
+  if ((size_t)Vp * npix * ds >= (1ull << 31) || (size_t)Vp * m * ds >= (1ull << 31))
+    return fail(ADMM_E_INVALID, "batch too large for 32-bit buffer offsets");
   C->P_fwd = ((C->g.n_det + kFwdRays - 1) / kFwdRays) * C->g.n_angles;
   C->P_edge = (int)((npix + kBlock * 4 - 1) / (kBlock * 4));
   RET(ensure(C->partH, (size_t)3 * V * C->P_back * 8));
@@ -517,7 +517,7 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   C->bound = true;
   if (C->use_graph) {
     auto fu = [&](hipStream_t s) {
-      return C->dtype == ADMM_DTYPE_F32 ? enqueue_update<float>(C, s) : enqueue_update<double>(C, s);
+      return C->dtype == ADMM_DTYPE_F32 ? enqueue_update_any<float>(C, s) : enqueue_update_any<double>(C, s);
     };
     RET(capture(C, fu, &C->g_update, &C->x_update));
     if (B.n_edges > 0) {
@@ -529,20 +529,29 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   return ADMM_OK;
 }
 
+extern "C++" {
+template <typename T>
+int batch_atb(admm_ctx* C, double* atb_out, hipStream_t s) {
+  const int V = C->b.V;
+  return with_vb(C->vb, [&](auto vbc) {
+    constexpr int VB = decltype(vbc)::value;
+    const int nch = (V + VB - 1) / VB;
+    hipLaunchKernelGGL((k_pack<T, VB>), dim3((C->mrays + 255) / 256, nch), dim3(256), 0, s, (const T*)C->b.b,
+                       (T*)C->bI.p, C->mrays, V);
+    CHECK_LAUNCH();
+    BackArgs<T> a{};
+    a.sino = (const T*)C->bI.p;
+    a.out_d = atb_out;
+    return launch_back<T, VB, BACK_ATB>(C, a, V, s);
+  });
+}
+}  // extern "C++"
+
 int admm_batch_atb(admm_ctx* C, double* atb_out, void* stream) {
   if (!C || !C->bound) return fail(ADMM_E_STATE, "no batch bound");
   if (!atb_out) return fail(ADMM_E_INVALID, "null atb_out");
   hipStream_t s = (hipStream_t)stream;
-  if (C->dtype == ADMM_DTYPE_F32) {
-    BackArgs<float> a{};
-    a.sino = (const float*)C->b.b;
-    a.out_d = atb_out;
-    return launch_back<float, BACK_ATB>(C, a, C->b.V, s);
-  }
-  BackArgs<double> a{};
-  a.sino = (const double*)C->b.b;
-  a.out_d = atb_out;
-  return launch_back<double, BACK_ATB>(C, a, C->b.V, s);
+  return C->dtype == ADMM_DTYPE_F32 ? batch_atb<float>(C, atb_out, s) : batch_atb<double>(C, atb_out, s);
 }
 
 int admm_node_update(admm_ctx* C, void* stream) {
@@ -552,7 +561,7 @@ int admm_node_update(admm_ctx* C, void* stream) {
     HIPCHK(hipGraphLaunch(C->x_update, s));
     return ADMM_OK;
   }
-  return C->dtype == ADMM_DTYPE_F32 ? enqueue_update<float>(C, s) : enqueue_update<double>(C, s);
+  return C->dtype == ADMM_DTYPE_F32 ? enqueue_update_any<float>(C, s) : enqueue_update_any<double>(C, s);
 }
 
 int admm_consensus(admm_ctx* C, void* stream) {
@@ -565,35 +574,35 @@ int admm_consensus(admm_ctx* C, void* stream) {
   return enqueue_consensus(C, s);
 }
 
+extern "C++" {
+template <typename T>
+int time_fwd(admm_ctx* C, int reps, hipStream_t s, float* ms) {
+  return with_vb(C->vb, [&](auto vbc) {
+    constexpr int VB = decltype(vbc)::value;
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    RET((launch_fwd<T, VB, 0>(C, (T*)C->xs.p, (T*)C->xsT.p, (T*)C->sino.p, nullptr, nullptr, C->b.V, s)));
+    HIPCHK(hipEventRecord(e0, s));
+    for (int i = 0; i < reps; ++i)
+      RET((launch_fwd<T, VB, 0>(C, (T*)C->xs.p, (T*)C->xsT.p, (T*)C->sino.p, nullptr, nullptr, C->b.V, s)));
+    HIPCHK(hipEventRecord(e1, s));
+    HIPCHK(hipEventSynchronize(e1));
+    HIPCHK(hipEventElapsedTime(ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return ADMM_OK;
+  });
+}
+}  // extern "C++"
+
 int admm_time_forward(admm_ctx* C, int reps, void* stream, double* ms_out) {
   if (!C || !C->bound) return fail(ADMM_E_STATE, "no batch bound");
   if (reps < 1 || !ms_out) return fail(ADMM_E_INVALID, "bad argument");
   hipStream_t s = (hipStream_t)stream;
-  hipEvent_t e0, e1;
-  HIPCHK(hipEventCreate(&e0));
-  HIPCHK(hipEventCreate(&e1));
-  // warm-up
-  if (C->dtype == ADMM_DTYPE_F32)
-    RET((launch_fwd<float, 0>(C, (float*)C->xs.p, (float*)C->xsT.p, (float*)C->sino.p, nullptr, nullptr, C->b.V, s)));
-  else
-    RET((launch_fwd<double, 0>(C, (double*)C->xs.p, (double*)C->xsT.p, (double*)C->sino.p, nullptr, nullptr, C->b.V,
-                               s)));
-  HIPCHK(hipEventRecord(e0, s));
-  for (int i = 0; i < reps; ++i) {
-    if (C->dtype == ADMM_DTYPE_F32)
-      RET((launch_fwd<float, 0>(C, (float*)C->xs.p, (float*)C->xsT.p, (float*)C->sino.p, nullptr, nullptr, C->b.V,
-                                s)));
-    else
-      RET((launch_fwd<double, 0>(C, (double*)C->xs.p, (double*)C->xsT.p, (double*)C->sino.p, nullptr, nullptr,
-                                 C->b.V, s)));
-  }
-  HIPCHK(hipEventRecord(e1, s));
-  HIPCHK(hipEventSynchronize(e1));
   float ms = 0.f;
-  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  RET(C->dtype == ADMM_DTYPE_F32 ? time_fwd<float>(C, reps, s, &ms) : time_fwd<double>(C, reps, s, &ms));
   *ms_out = (double)ms / reps;
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   return ADMM_OK;
 }
 

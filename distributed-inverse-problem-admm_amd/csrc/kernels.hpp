@@ -1,27 +1,34 @@
 // kernels.hpp -- CDNA4 (gfx950) kernels of the decentralized-ADMM tomography hot path.
 //
-// Everything is batched over the graph nodes this GPU owns ("node batch"):
-// all nodes share one parallel-beam geometry (block_2_load_odl_data.py:51,
-// every node spans [0, pi) with its own a angles), so one launch projects
-// VB node images at once and the per-step geometry (interpolation position,
-// weights, clamped offsets) is computed once and reused VB times.
+// Everything is batched over the graph nodes this GPU owns.  All nodes share one
+// parallel-beam geometry (block_2_load_odl_data.py:69: every node spans [0, pi)
+// with its own a angles), so one launch projects VB node images at once: the
+// per-step geometry (interpolation position, weights, clamped offsets) is computed
+// once and reused VB times.
 //
-// Numerics (see DESIGN.md "Numerics"):
-//   * projector inputs/outputs ("samples") are T = float (C2-C4) or double (C5);
-//   * interpolation positions are evaluated in float64 so the operator matches
-//     the float64 oracle to ~1e-7 (a float32 position has 3e-5 absolute error at N=512);
-//   * the CG solution x, residual r, split-Bregman d/e and edge state y/z are float64;
-//   * every reduction is a fixed-order tree over fixed partial slots:
-//     bitwise reproducible, independent of how many GPUs hold the graph.
+// "Sample" buffers (projector inputs / outputs: p, p^T, Hp, x_s, sinograms) are
+// node-interleaved:  element (node v, pixel-or-ray q) lives at
+//     [(v / VB) * L + q] * VB + (v % VB)          (L = pixels or rays)
+// so a tap loads the VB nodes' values of one pixel with 16-byte vector loads
+// (buffer_load_dwordx4) instead of VB separate dword loads.  VB = 1 is the plain
+// node-major layout (operator API).  Solver state (x, r, d, e, y, z, q) is float64
+// node-major [V][n].
+//
+// Numerics (DESIGN.md "Numerics"):
+//   * samples are T = float (C2-C4) or double (C5);
+//   * interpolation positions are evaluated in float64 (a float32 position has
+//     3e-5 absolute error at N = 512, which would perturb the operator ~1e-5);
+//   * x, r, d, e, y, z are float64;
+//   * every reduction is a fixed-order tree over fixed partial slots: bitwise
+//     reproducible and independent of how the graph is sharded over GPUs.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace admm {
 
-constexpr int kWave = 64;
 constexpr int kBlock = 256;
-constexpr int kTile = 64;        // elementwise / transposing kernels: 64x64 pixel tiles
+constexpr int kTile = 32;        // elementwise / transposing kernels: 32x32 pixel tiles, block 32 x 8
 constexpr int kBackTileJ = 64;   // back-projector block: 64 (j) x 4 (i) pixels
 constexpr int kBackTileI = 4;
 constexpr int kFwdRays = 64;     // forward-projector block: 64 rays x 4 step segments
@@ -32,38 +39,69 @@ constexpr int kAngChunk = 256;   // back-projector angle table chunk staged in L
 // Ray (t,k), step m:  l = A0 + k*A1 + m*dl  (interpolation coordinate).
 struct FwdAngle {
   double A0, A1, dl;
-  float L;    // path length per step h/|alpha|
+  double L;   // path length per step h/|alpha|
   int caseA;  // 1: step over axis-1 index on the transposed image
+  int pad;
 };
 // Per-angle back-projector constants: fractional bin k_f = B0 + i*Bi + j*Bj,
 // weight(k) = max(0, 1 - |k-k_f|*slope) * L.
 struct BackAngle {
   double B0, Bi, Bj;
-  float slope, L;
+  double slope, L;
 };
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
 
 // ---------------------------------------------------------------------------
-// buffer loads: one 128-bit resource per array, 32-bit per-lane byte offsets,
-// per-node offsets in an SGPR (soffset) -> no per-lane 64-bit address math.
+// vector I/O of VB samples (VB*sizeof(T) contiguous bytes)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
 }
-template <typename T>
-__device__ __forceinline__ T bload(__amdgpu_buffer_rsrc_t r, int voff, int soff);
-template <>
-__device__ __forceinline__ float bload<float>(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+
+template <typename T, int VB>
+__device__ __forceinline__ void vload(__amdgpu_buffer_rsrc_t r, int voff, int soff, T (&o)[VB]) {
+  constexpr int BYTES = VB * (int)sizeof(T);
+  if constexpr (BYTES >= 16) {
+    constexpr int PER = 16 / (int)sizeof(T);
+#pragma unroll
+    for (int q = 0; q < BYTES / 16; ++q) {
+      auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16 * q, soff, 0);
+      T t[PER];
+      __builtin_memcpy(t, &v, 16);
+#pragma unroll
+      for (int e = 0; e < PER; ++e) o[q * PER + e] = t[e];
+    }
+  } else if constexpr (BYTES == 8) {
+    auto v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+    __builtin_memcpy(o, &v, 8);
+  } else {
+    auto v = __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
+    __builtin_memcpy(o, &v, 4);
+  }
 }
-template <>
-__device__ __forceinline__ double bload<double>(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+
+template <typename T, int VB>
+struct alignas((VB * sizeof(T)) >= 16 ? 16 : (VB * sizeof(T))) Pack {
+  T v[VB];
+};
+
+template <typename T, int VB>
+__device__ __forceinline__ void gload(const T* __restrict__ p, T (&o)[VB]) {
+  const Pack<T, VB> k = *reinterpret_cast<const Pack<T, VB>*>(p);
+#pragma unroll
+  for (int u = 0; u < VB; ++u) o[u] = k.v[u];
+}
+template <typename T, int VB>
+__device__ __forceinline__ void gstore(T* __restrict__ p, const T (&o)[VB]) {
+  Pack<T, VB> k;
+#pragma unroll
+  for (int u = 0; u < VB; ++u) k.v[u] = o[u];
+  *reinterpret_cast<Pack<T, VB>*>(p) = k;
 }
 
 // ---------------------------------------------------------------------------
-// deterministic block reduction of NQ float64 values per thread (256 threads)
+// deterministic block reduction of NQ float64 values per thread (256 threads);
 // result valid in thread 0.  Fixed shuffle tree + fixed LDS order.
 // ---------------------------------------------------------------------------
 template <int NQ>
@@ -96,9 +134,10 @@ __device__ __forceinline__ void block_reduce(double (&v)[NQ], double* lds /* >= 
 // Block = 64 consecutive detector bins of one angle x 4 step segments (one wave each).
 // Lanes are consecutive rays, so at every step a wave reads one contiguous row segment:
 // case-B angles read img (row m = axis-0 index), case-A angles read the transposed
-// copy imgT (row m = axis-1 index) -- both coalesced.  The 4 segment partial sums
-// are combined in LDS in fixed order.
-// MODE 0: store A x.   MODE 1: store s = A x - b and per-block partials of ||s||^2.
+// copy imgT (row m = axis-1 index).  Each tap is one VB-vector load (VB nodes).
+// The 4 segment partial sums are combined in LDS in fixed order.
+// MODE 0: store A x (interleaved).
+// MODE 1: store s = A x - b (interleaved; b node-major [V][m]) and partials of ||s||^2.
 // ===========================================================================
 template <typename T, int VB, int MODE>
 __global__ __launch_bounds__(kBlock) void k_fwd(const T* __restrict__ img, const T* __restrict__ imgT,
@@ -109,12 +148,15 @@ __global__ __launch_bounds__(kBlock) void k_fwd(const T* __restrict__ img, const
   const int seg = threadIdx.x >> 6;
   const int k = blockIdx.x * kFwdRays + lane;
   const int t = blockIdx.y;
-  const int v0 = blockIdx.z * VB;
+  const int chunk = blockIdx.z;
+  const int v0 = chunk * VB;
   const int nv = min(VB, V - v0);
   const int npix = N * N;
+  const int nch = (V + VB - 1) / VB;
   const FwdAngle a = ang[t];
   const T* src = a.caseA ? imgT : img;
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc(src, (uint32_t)((size_t)V * npix * sizeof(T)));
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(src, (uint32_t)((size_t)nch * npix * VB * sizeof(T)));
+  const int soff = chunk * npix * VB * (int)sizeof(T);
   T acc[VB];
 #pragma unroll
   for (int u = 0; u < VB; ++u) acc[u] = T(0);
@@ -144,17 +186,15 @@ __global__ __launch_bounds__(kBlock) void k_fwd(const T* __restrict__ img, const
       w0 = (i0 >= 0 && i0 <= N - 1) ? w0 : T(0);
       w1 = (i0 >= -1 && i0 <= N - 2) ? w1 : T(0);
       const int row = m * N;
-      const int o0 = (row + clampi(i0, 0, N - 1)) * (int)sizeof(T);
-      const int o1 = (row + clampi(i0 + 1, 0, N - 1)) * (int)sizeof(T);
+      const int o0 = (row + clampi(i0, 0, N - 1)) * VB * (int)sizeof(T);
+      const int o1 = (row + clampi(i0 + 1, 0, N - 1)) * VB * (int)sizeof(T);
+      T p0[VB], p1[VB];
+      vload<T, VB>(rs, o0, soff, p0);
+      vload<T, VB>(rs, o1, soff, p1);
 #pragma unroll
       for (int u = 0; u < VB; ++u) {
-        if (u < nv) {
-          const int so = (v0 + u) * npix * (int)sizeof(T);
-          const T p0 = bload<T>(rs, o0, so);
-          const T p1 = bload<T>(rs, o1, so);
-          acc[u] = fma(w0, p0, acc[u]);
-          acc[u] = fma(w1, p1, acc[u]);
-        }
+        acc[u] = fma(w0, p0[u], acc[u]);
+        acc[u] = fma(w1, p1[u], acc[u]);
       }
     }
   }
@@ -166,18 +206,21 @@ __global__ __launch_bounds__(kBlock) void k_fwd(const T* __restrict__ img, const
 #pragma unroll
   for (int u = 0; u < VB; ++u) sq[u] = 0.0;
   if (seg == 0 && k < n_det) {
+    const size_t ray = (size_t)t * n_det + k;
+    T s[VB];
 #pragma unroll
     for (int u = 0; u < VB; ++u) {
-      if (u < nv) {
-        T s = ((red[0][u][lane] + red[1][u][lane]) + (red[2][u][lane] + red[3][u][lane])) * (T)a.L;
-        const size_t o = (size_t)(v0 + u) * n_ang * n_det + (size_t)t * n_det + k;
-        if (MODE == 1) {
-          s = s - bsino[o];
-          sq[u] = (double)s * (double)s;
+      s[u] = ((red[0][u][lane] + red[1][u][lane]) + (red[2][u][lane] + red[3][u][lane])) * (T)a.L;
+      if (MODE == 1) {
+        if (u < nv) {
+          s[u] = s[u] - bsino[(size_t)(v0 + u) * n_ang * n_det + ray];
+          sq[u] = (double)s[u] * (double)s[u];
+        } else {
+          s[u] = T(0);
         }
-        sino[o] = s;
       }
     }
+    gstore<T, VB>(sino + ((size_t)chunk * n_ang * n_det + ray) * VB, s);
   }
   if (MODE == 1) {
     __syncthreads();
@@ -199,11 +242,11 @@ __global__ __launch_bounds__(kBlock) void k_fwd(const T* __restrict__ img, const
 // Replaces `Ai.T @ r` (block_6_admm_loop_ver2.py:145).  No atomics: each pixel
 // gathers its <= 2 bins per angle.  The angle table is staged in LDS.
 // Fused epilogues (MODE):
-//   BACK_PLAIN : out = A^T s                                   (operator API)
-//   BACK_ATB   : atb = A^T b (float64)                          (setup)
-//   BACK_WSQ   : W = max(sum_r A[r,p]^2, 1e-12) (float64)       (make_precisions, block_3:20-23)
-//   BACK_H     : Hp = A^T A p + rho D p + mu K^T K p; partials p.Hp, r.Hp, Hp.Hp  (CG)
-//   BACK_INIT  : r = A^T b + rho c + mu K^T(d-e) - H xs;  p = r; partial r.r   (CG start)
+//   BACK_PLAIN : out = A^T s  (interleaved samples)                  (operator API)
+//   BACK_ATB   : atb = A^T b (float64 node-major)                    (setup)
+//   BACK_WSQ   : W = max(sum_r A[r,p]^2, 1e-12) (float64)            (make_precisions, block_3:20-23)
+//   BACK_H     : Hp = A^T A p + rho D p + mu K^T K p; partials p.Hp, r.Hp, Hp.Hp      (CG)
+//   BACK_INIT  : r = A^T b + rho c + mu K^T(d-e) - H xs;  p = r; partial r.r         (CG start)
 //   BACK_DIAG  : g = A^T s + rho (D x - c) + lam K^T sub(Kx); partials |g|^2, TV(x),
 //                sum_j rho/2 q_ij (x - v_ij)^2, |x - phantom|^2   (block_6_ver2.py:135-149)
 // ===========================================================================
@@ -211,16 +254,16 @@ enum BackMode { BACK_PLAIN = 0, BACK_ATB = 1, BACK_WSQ = 2, BACK_H = 3, BACK_INI
 
 template <typename T>
 struct BackArgs {
-  const T* sino;            // [V][m]
+  const T* sino;            // interleaved [C][m][VB]
   const BackAngle* ang;     // [n_ang]
   int N, n_det, n_ang, V;
   // outputs
-  T* out_t;                 // PLAIN: [V][n];  H: Hp [V][n];  INIT: p [V][n]
-  double* out_d;            // ATB: atb;  WSQ: W;  INIT: r
+  T* out_t;                 // PLAIN: A^T s;  H: Hp;  INIT: p   (interleaved)
+  double* out_d;            // ATB: atb;  WSQ: W;  INIT: r     (float64 node-major)
   double* part;             // [V][NQ][P]
   // epilogue inputs
-  const T* pin;             // H: p;  INIT: xs (sample copy of x)
-  const double* r;          // H: r (float64 residual)
+  const T* pin;             // H: p;  INIT: xs (interleaved)
+  const double* r;          // H: r
   const double* dsum;       // [V][n]
   const double* atb;        // INIT
   const double* cvec;       // INIT, DIAG: c = sum_j q v
@@ -263,18 +306,6 @@ __device__ __forceinline__ void tv_sub(double gx, double gy, int kind, double& p
   }
 }
 
-template <typename T>
-__device__ __forceinline__ double ktk_at(const T* __restrict__ p, int N, int i, int j) {
-  // (K^T K p)[i,j] with Neumann (zero last-difference) boundary
-  const double c = (double)p[i * N + j];
-  double s = 0.0;
-  if (i >= 1) s += c - (double)p[(i - 1) * N + j];
-  if (i <= N - 2) s -= (double)p[(i + 1) * N + j] - c;
-  if (j >= 1) s += c - (double)p[i * N + j - 1];
-  if (j <= N - 2) s -= (double)p[i * N + j + 1] - c;
-  return s;
-}
-
 // (K^T w)[i,j] for a two-component float64 field w = d - e stored [2][n]
 __device__ __forceinline__ double kt_w_at(const double* __restrict__ d, const double* __restrict__ e, int N,
                                           int i, int j) {
@@ -290,17 +321,20 @@ __device__ __forceinline__ double kt_w_at(const double* __restrict__ d, const do
 
 template <typename T, int VB, int MODE>
 __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
-  constexpr int NQ = (MODE == BACK_H) ? 3 : (MODE == BACK_INIT) ? 1 : (MODE == BACK_DIAG) ? 4 : 1;
+  constexpr int NQ = (MODE == BACK_H) ? 3 : (MODE == BACK_DIAG) ? 4 : 1;
   const int N = A.N, n_det = A.n_det, n_ang = A.n_ang;
   const int npix = N * N;
   const int m_rays = n_ang * n_det;
   const int j = blockIdx.x * kBackTileJ + (threadIdx.x & 63);
   const int i = blockIdx.y * kBackTileI + (threadIdx.x >> 6);
   const bool inb = (i < N) && (j < N);
-  const int v0 = blockIdx.z * VB;
+  const int chunk = blockIdx.z;
+  const int v0 = chunk * VB;
   const int nv = (MODE == BACK_WSQ) ? 1 : min(VB, A.V - v0);
+  const int nch = (A.V + VB - 1) / VB;
   const __amdgpu_buffer_rsrc_t rs =
-      make_rsrc(A.sino, (uint32_t)((size_t)A.V * m_rays * sizeof(T)));
+      make_rsrc(A.sino, (uint32_t)((size_t)nch * m_rays * VB * sizeof(T)));
+  const int soff = chunk * m_rays * VB * (int)sizeof(T);
 
   __shared__ BackAngle sang[kAngChunk];
   T acc[VB];
@@ -329,17 +363,15 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
           acc[0] = fma(w1, w1, acc[0]);
         } else {
           const int rowo = (t0 + tt) * n_det;
-          const int o0 = (rowo + clampi(k0, 0, n_det - 1)) * (int)sizeof(T);
-          const int o1 = (rowo + clampi(k0 + 1, 0, n_det - 1)) * (int)sizeof(T);
+          const int o0 = (rowo + clampi(k0, 0, n_det - 1)) * VB * (int)sizeof(T);
+          const int o1 = (rowo + clampi(k0 + 1, 0, n_det - 1)) * VB * (int)sizeof(T);
+          T s0[VB], s1[VB];
+          vload<T, VB>(rs, o0, soff, s0);
+          vload<T, VB>(rs, o1, soff, s1);
 #pragma unroll
           for (int u = 0; u < VB; ++u) {
-            if (u < nv) {
-              const int so = (v0 + u) * m_rays * (int)sizeof(T);
-              const T s0 = bload<T>(rs, o0, so);
-              const T s1 = bload<T>(rs, o1, so);
-              acc[u] = fma(w0, s0, acc[u]);
-              acc[u] = fma(w1, s1, acc[u]);
-            }
+            acc[u] = fma(w0, s0[u], acc[u]);
+            acc[u] = fma(w1, s1[u], acc[u]);
           }
         }
       }
@@ -348,12 +380,9 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
 
   // ---------------- fused epilogues ----------------
   const int pix = i * N + j;
+  const size_t sbase = (size_t)chunk * npix * VB;  // interleaved sample base of this chunk
   if (MODE == BACK_PLAIN) {
-    if (inb) {
-#pragma unroll
-      for (int u = 0; u < VB; ++u)
-        if (u < nv) A.out_t[(size_t)(v0 + u) * npix + pix] = acc[u];
-    }
+    if (inb) gstore<T, VB>(A.out_t + sbase + (size_t)pix * VB, acc);
     return;
   }
   if (MODE == BACK_ATB) {
@@ -376,31 +405,66 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
     for (int q = 0; q < NQ; ++q) pq[u][q] = 0.0;
 
   if (inb) {
+    if constexpr (MODE == BACK_H || MODE == BACK_INIT) {
+      // H v = acc + rho D v + mu K^T K v  (v = p or xs, interleaved samples)
+      const T* pv = A.pin + sbase;
+      T pc[VB], pn[VB];
+      double ktk[VB];
+      gload<T, VB>(pv + (size_t)pix * VB, pc);
 #pragma unroll
-    for (int u = 0; u < VB; ++u) {
-      if (u >= nv) continue;
-      const int v = v0 + u;
-      const size_t vo = (size_t)v * npix;
-      if (MODE == BACK_H || MODE == BACK_INIT) {
-        const T* pv = A.pin + vo;
-        const double pc = (double)pv[pix];
-        const double h = (double)acc[u] + A.rho * A.dsum[vo + pix] * pc + A.mu * ktk_at<T>(pv, N, i, j);
-        if (MODE == BACK_H) {
-          const T hp = (T)h;
-          A.out_t[vo + pix] = hp;
-          const double hd = (double)hp;
-          pq[u][0] = pc * hd;
-          pq[u][1] = A.r[vo + pix] * hd;
-          pq[u][2] = hd * hd;
-        } else {
-          const double* dv = A.dvar + 2 * vo;
-          const double* ev = A.evar + 2 * vo;
-          const double rr = A.atb[vo + pix] + A.rho * A.cvec[vo + pix] + A.mu * kt_w_at(dv, ev, N, i, j) - h;
-          A.out_d[vo + pix] = rr;
-          A.out_t[vo + pix] = (T)rr;
-          pq[u][0] = rr * rr;
+      for (int u = 0; u < VB; ++u) ktk[u] = 0.0;
+      if (i >= 1) {
+        gload<T, VB>(pv + (size_t)(pix - N) * VB, pn);
+#pragma unroll
+        for (int u = 0; u < VB; ++u) ktk[u] += (double)pc[u] - (double)pn[u];
+      }
+      if (i <= N - 2) {
+        gload<T, VB>(pv + (size_t)(pix + N) * VB, pn);
+#pragma unroll
+        for (int u = 0; u < VB; ++u) ktk[u] -= (double)pn[u] - (double)pc[u];
+      }
+      if (j >= 1) {
+        gload<T, VB>(pv + (size_t)(pix - 1) * VB, pn);
+#pragma unroll
+        for (int u = 0; u < VB; ++u) ktk[u] += (double)pc[u] - (double)pn[u];
+      }
+      if (j <= N - 2) {
+        gload<T, VB>(pv + (size_t)(pix + 1) * VB, pn);
+#pragma unroll
+        for (int u = 0; u < VB; ++u) ktk[u] -= (double)pn[u] - (double)pc[u];
+      }
+      T outv[VB];
+#pragma unroll
+      for (int u = 0; u < VB; ++u) {
+        outv[u] = T(0);
+        if (u < nv) {
+          const size_t vo = (size_t)(v0 + u) * npix;
+          const double pcd = (double)pc[u];
+          const double h = (double)acc[u] + A.rho * A.dsum[vo + pix] * pcd + A.mu * ktk[u];
+          if constexpr (MODE == BACK_H) {
+            const T hp = (T)h;
+            outv[u] = hp;
+            const double hd = (double)hp;
+            pq[u][0] = pcd * hd;
+            pq[u][1] = A.r[vo + pix] * hd;
+            pq[u][2] = hd * hd;
+          } else {
+            const double* dv = A.dvar + 2 * vo;
+            const double* ev = A.evar + 2 * vo;
+            const double rr = A.atb[vo + pix] + A.rho * A.cvec[vo + pix] + A.mu * kt_w_at(dv, ev, N, i, j) - h;
+            A.out_d[vo + pix] = rr;
+            outv[u] = (T)rr;
+            pq[u][0] = rr * rr;
+          }
         }
-      } else if (MODE == BACK_DIAG) {
+      }
+      gstore<T, VB>(A.out_t + sbase + (size_t)pix * VB, outv);
+    } else if constexpr (MODE == BACK_DIAG) {
+#pragma unroll
+      for (int u = 0; u < VB; ++u) {
+        if (u >= nv) continue;
+        const int v = v0 + u;
+        const size_t vo = (size_t)v * npix;
         const double* xv = A.x + vo;
         const double xc = xv[pix];
         // lam * K^T sub(Kx) at (i,j): needs the subgradient at (i,j), (i-1,j), (i,j-1)
@@ -460,107 +524,144 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
 }
 
 // ===========================================================================
-// 64x64-tile elementwise kernels (block 256 = 64 x 4, 16 rows per thread).
-// Each writes its "sample" output both row-major and transposed (LDS tile),
-// because the forward projector reads the transposed copy for case-A angles.
+// 32x32-tile elementwise kernels (block 256 = 32 (j) x 8 (i), rows ty + 8r).
+// Sample outputs are written row-major AND transposed (through an LDS tile of
+// VB-vectors), because the forward projector reads the transposed copy for
+// case-A angles.  blockIdx.z = node chunk.
 // ===========================================================================
-template <typename T>
-__device__ __forceinline__ void tile_store_T(T (&tl)[kTile][kTile + 1], T* __restrict__ outT, int N, int i0,
-                                             int j0) {
+template <typename T, int VB>
+struct TileT {
+  Pack<T, VB> t[kTile][kTile + 1];
+};
+
+template <typename T, int VB>
+__device__ __forceinline__ void tile_put(TileT<T, VB>& tl, int r, int c, const T (&v)[VB]) {
+#pragma unroll
+  for (int u = 0; u < VB; ++u) tl.t[r][c].v[u] = v[u];
+}
+
+// outT (interleaved, chunk base applied by caller): outT[j][i] = tile[i - i0][j - j0]
+template <typename T, int VB>
+__device__ __forceinline__ void tile_store_T(TileT<T, VB>& tl, T* __restrict__ outT, int N, int i0, int j0) {
   __syncthreads();
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  // outT[j][i] = tile[i-i0][j-j0]
-  for (int r = ty; r < kTile; r += 4) {
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int r = ty; r < kTile; r += 8) {
     const int jj = j0 + r, ii = i0 + tx;
-    if (jj < N && ii < N) outT[(size_t)jj * N + ii] = tl[tx][r];
+    if (jj < N && ii < N) *reinterpret_cast<Pack<T, VB>*>(outT + ((size_t)jj * N + ii) * VB) = tl.t[tx][r];
   }
 }
 
 // gather (prologue of the x-update, block_6_admm_loop_ver2.py:85-95,137-140):
 //   c_v = sum_{e in inc(v)} q_e (z_e - sign * y_e);  xs = (T) x, xsT = xs^T
-template <typename T>
+template <typename T, int VB>
 __global__ __launch_bounds__(kBlock) void k_gather(const double* __restrict__ x, const double* __restrict__ y,
                                                    const double* __restrict__ z, const double* __restrict__ q,
                                                    const int* __restrict__ inc_off, const int* __restrict__ inc_edge,
                                                    const int* __restrict__ inc_qslot,
                                                    const int* __restrict__ inc_sign, double* __restrict__ c,
-                                                   T* __restrict__ xs, T* __restrict__ xsT, int N) {
-  __shared__ T tl[kTile][kTile + 1];
-  const int v = blockIdx.z;
+                                                   T* __restrict__ xs, T* __restrict__ xsT, int N, int V) {
+  __shared__ TileT<T, VB> tl;
+  const int chunk = blockIdx.z, v0 = chunk * VB, nv = min(VB, V - v0);
   const int npix = N * N;
+  const size_t sbase = (size_t)chunk * npix * VB;
   const int i0 = blockIdx.y * kTile, j0 = blockIdx.x * kTile;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int e0 = inc_off[v], e1 = inc_off[v + 1];
-  const size_t vo = (size_t)v * npix;
-  for (int r = ty; r < kTile; r += 4) {
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int r = ty; r < kTile; r += 8) {
     const int i = i0 + r, j = j0 + tx;
     if (i < N && j < N) {
       const int pix = i * N + j;
-      double acc = 0.0;
-      for (int qq = e0; qq < e1; ++qq) {
-        const size_t eo = (size_t)inc_edge[qq] * npix + pix;
-        const double vij = z[eo] - (double)inc_sign[qq] * y[eo];
-        acc += q[(size_t)inc_qslot[qq] * npix + pix] * vij;
+      T s[VB];
+#pragma unroll
+      for (int u = 0; u < VB; ++u) {
+        s[u] = T(0);
+        if (u < nv) {
+          const int v = v0 + u;
+          double acc = 0.0;
+          for (int qq = inc_off[v]; qq < inc_off[v + 1]; ++qq) {
+            const size_t eo = (size_t)inc_edge[qq] * npix + pix;
+            const double vij = z[eo] - (double)inc_sign[qq] * y[eo];
+            acc += q[(size_t)inc_qslot[qq] * npix + pix] * vij;
+          }
+          c[(size_t)v * npix + pix] = acc;
+          s[u] = (T)x[(size_t)v * npix + pix];
+        }
       }
-      c[vo + pix] = acc;
-      const T s = (T)x[vo + pix];
-      xs[vo + pix] = s;
-      tl[r][tx] = s;
+      gstore<T, VB>(xs + sbase + (size_t)pix * VB, s);
+      tile_put<T, VB>(tl, r, tx, s);
     }
   }
-  tile_store_T<T>(tl, xsT + vo, N, i0, j0);
+  tile_store_T<T, VB>(tl, xsT + sbase, N, i0, j0);
 }
 
-template <typename T>
+template <typename T, int VB>
 __global__ __launch_bounds__(kBlock) void k_transpose(const T* __restrict__ in, T* __restrict__ outT, int N) {
-  __shared__ T tl[kTile][kTile + 1];
-  const int v = blockIdx.z;
-  const size_t vo = (size_t)v * N * N;
+  __shared__ TileT<T, VB> tl;
+  const size_t sbase = (size_t)blockIdx.z * N * N * VB;
   const int i0 = blockIdx.y * kTile, j0 = blockIdx.x * kTile;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  for (int r = ty; r < kTile; r += 4) {
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int r = ty; r < kTile; r += 8) {
     const int i = i0 + r, j = j0 + tx;
-    if (i < N && j < N) tl[r][tx] = in[vo + (size_t)i * N + j];
+    if (i < N && j < N) tl.t[r][tx] = *reinterpret_cast<const Pack<T, VB>*>(in + sbase + ((size_t)i * N + j) * VB);
   }
-  tile_store_T<T>(tl, outT + vo, N, i0, j0);
+  tile_store_T<T, VB>(tl, outT + sbase, N, i0, j0);
 }
 
-// CG step with the single-reduction identity (see oracle/node_solver.py):
+// CG step with the single-reduction identity (oracle/node_solver.py):
 //   alpha = rr/pHp, rr' = rr - 2 alpha rHp + alpha^2 HpHp, beta = rr'/rr
 //   x += alpha p;  r -= alpha Hp;  p = r + beta p  (p also written transposed)
-template <typename T>
+template <typename T, int VB>
 __global__ __launch_bounds__(kBlock) void k_cg_update(double* __restrict__ x, double* __restrict__ r,
                                                       T* __restrict__ p, T* __restrict__ pT,
                                                       const T* __restrict__ Hp, const double* __restrict__ redH,
                                                       const double* __restrict__ rr_in, double* __restrict__ rr_out,
-                                                      int N) {
-  __shared__ T tl[kTile][kTile + 1];
-  const int v = blockIdx.z;
-  const double pHp = redH[3 * v + 0], rHp = redH[3 * v + 1], HH = redH[3 * v + 2];
-  const double rr = rr_in[v];
-  const double alpha = (pHp != 0.0) ? rr / pHp : 0.0;
-  double rrn = rr - 2.0 * alpha * rHp + alpha * alpha * HH;
-  rrn = fmax(rrn, 0.0);
-  const double beta = (rr != 0.0) ? rrn / rr : 0.0;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) rr_out[v] = rrn;
-  const size_t vo = (size_t)v * N * N;
-  const int i0 = blockIdx.y * kTile, j0 = blockIdx.x * kTile;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  for (int rw = ty; rw < kTile; rw += 4) {
-    const int i = i0 + rw, j = j0 + tx;
-    if (i < N && j < N) {
-      const size_t o = vo + (size_t)i * N + j;
-      const double pv = (double)p[o];
-      const double hv = (double)Hp[o];
-      x[o] += alpha * pv;
-      const double rn = r[o] - alpha * hv;
-      r[o] = rn;
-      const T np = (T)(rn + beta * pv);
-      p[o] = np;
-      tl[rw][tx] = np;
+                                                      int N, int V) {
+  __shared__ TileT<T, VB> tl;
+  const int chunk = blockIdx.z, v0 = chunk * VB, nv = min(VB, V - v0);
+  const int npix = N * N;
+  const size_t sbase = (size_t)chunk * npix * VB;
+  double alpha[VB], beta[VB];
+#pragma unroll
+  for (int u = 0; u < VB; ++u) {
+    alpha[u] = 0.0;
+    beta[u] = 0.0;
+    if (u < nv) {
+      const int v = v0 + u;
+      const double pHp = redH[3 * v + 0], rHp = redH[3 * v + 1], HH = redH[3 * v + 2];
+      const double rr = rr_in[v];
+      const double al = (pHp != 0.0) ? rr / pHp : 0.0;
+      double rrn = rr - 2.0 * al * rHp + al * al * HH;
+      rrn = fmax(rrn, 0.0);
+      alpha[u] = al;
+      beta[u] = (rr != 0.0) ? rrn / rr : 0.0;
+      if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) rr_out[v] = rrn;
     }
   }
-  tile_store_T<T>(tl, pT + vo, N, i0, j0);
+  const int i0 = blockIdx.y * kTile, j0 = blockIdx.x * kTile;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int rw = ty; rw < kTile; rw += 8) {
+    const int i = i0 + rw, j = j0 + tx;
+    if (i < N && j < N) {
+      const int pix = i * N + j;
+      T pv[VB], hv[VB], np[VB];
+      gload<T, VB>(p + sbase + (size_t)pix * VB, pv);
+      gload<T, VB>(Hp + sbase + (size_t)pix * VB, hv);
+#pragma unroll
+      for (int u = 0; u < VB; ++u) {
+        np[u] = T(0);
+        if (u < nv) {
+          const size_t o = (size_t)(v0 + u) * npix + pix;
+          const double pd = (double)pv[u];
+          x[o] += alpha[u] * pd;
+          const double rn = r[o] - alpha[u] * (double)hv[u];
+          r[o] = rn;
+          np[u] = (T)(rn + beta[u] * pd);
+        }
+      }
+      gstore<T, VB>(p + sbase + (size_t)pix * VB, np);
+      tile_put<T, VB>(tl, rw, tx, np);
+    }
+  }
+  tile_store_T<T, VB>(tl, pT + sbase, N, i0, j0);
 }
 
 // split-Bregman (d, e) update after a CG solve:
@@ -581,76 +682,101 @@ __device__ __forceinline__ void shrink2(double ux, double uy, double tau, int ki
   }
 }
 
-template <typename T, bool LAST>
+template <typename T, int VB, bool LAST>
 __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__ x, const double* __restrict__ din,
                                                       const double* __restrict__ ein, double* __restrict__ dout,
                                                       double* __restrict__ eout, double* __restrict__ r,
                                                       T* __restrict__ p, T* __restrict__ pT,
                                                       double* __restrict__ part, double tau, double mu, int kind,
-                                                      int N) {
-  __shared__ T tl[kTile][kTile + 1];
-  __shared__ double lds[4];
-  const int v = blockIdx.z;
+                                                      int N, int V) {
+  __shared__ TileT<T, VB> tl;
+  __shared__ double lds[4 * VB];
+  const int chunk = blockIdx.z, v0 = chunk * VB, nv = min(VB, V - v0);
   const int npix = N * N;
-  const size_t vo = (size_t)v * npix;
-  const double* xv = x + vo;
-  const double* dv = din + 2 * vo;
-  const double* ev = ein + 2 * vo;
+  const size_t sbase = (size_t)chunk * npix * VB;
   const int i0 = blockIdx.y * kTile, j0 = blockIdx.x * kTile;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  double rrp = 0.0;
-  for (int rw = ty; rw < kTile; rw += 4) {
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  double rrp[VB];
+#pragma unroll
+  for (int u = 0; u < VB; ++u) rrp[u] = 0.0;
+  for (int rw = ty; rw < kTile; rw += 8) {
     const int i = i0 + rw, j = j0 + tx;
     if (i >= N || j >= N) continue;
     const int o = i * N + j;
-    double gx, gy, ux, uy, ndx, ndy;
-    grad_at(xv, N, i, j, gx, gy);
-    ux = gx + ev[o];
-    uy = gy + ev[npix + o];
-    shrink2(ux, uy, tau, kind, ndx, ndy);
-    const double nex = ux - ndx, ney = uy - ndy;
-    dout[2 * vo + o] = ndx;
-    dout[2 * vo + npix + o] = ndy;
-    eout[2 * vo + o] = nex;
-    eout[2 * vo + npix + o] = ney;
-    T s;
-    if (!LAST) {
-      // K^T(dw) at (i,j): dw_x(i-1,j) - dw_x(i,j) + dw_y(i,j-1) - dw_y(i,j)
-      double kt = 0.0;
-      if (i <= N - 2) kt -= (ndx - nex) - (dv[o] - ev[o]);
-      if (j <= N - 2) kt -= (ndy - ney) - (dv[npix + o] - ev[npix + o]);
-      if (i >= 1) {
-        const int oo = o - N;
-        double ax, ay, bx, by;
-        grad_at(xv, N, i - 1, j, ax, ay);
-        const double vx = ax + ev[oo], vy = ay + ev[npix + oo];
-        shrink2(vx, vy, tau, kind, bx, by);
-        kt += (bx - (vx - bx)) - (dv[oo] - ev[oo]);
+    T sv[VB];
+#pragma unroll
+    for (int u = 0; u < VB; ++u) {
+      sv[u] = T(0);
+      if (u >= nv) continue;
+      const size_t vo = (size_t)(v0 + u) * npix;
+      const double* xv = x + vo;
+      const double* dv = din + 2 * vo;
+      const double* ev = ein + 2 * vo;
+      double gx, gy, ux, uy, ndx, ndy;
+      grad_at(xv, N, i, j, gx, gy);
+      ux = gx + ev[o];
+      uy = gy + ev[npix + o];
+      shrink2(ux, uy, tau, kind, ndx, ndy);
+      const double nex = ux - ndx, ney = uy - ndy;
+      dout[2 * vo + o] = ndx;
+      dout[2 * vo + npix + o] = ndy;
+      eout[2 * vo + o] = nex;
+      eout[2 * vo + npix + o] = ney;
+      if (!LAST) {
+        // K^T(dw) at (i,j): dw_x(i-1,j) - dw_x(i,j) + dw_y(i,j-1) - dw_y(i,j)
+        double kt = 0.0;
+        if (i <= N - 2) kt -= (ndx - nex) - (dv[o] - ev[o]);
+        if (j <= N - 2) kt -= (ndy - ney) - (dv[npix + o] - ev[npix + o]);
+        if (i >= 1) {
+          const int oo = o - N;
+          double ax, ay, bx, by;
+          grad_at(xv, N, i - 1, j, ax, ay);
+          const double vx = ax + ev[oo], vy = ay + ev[npix + oo];
+          shrink2(vx, vy, tau, kind, bx, by);
+          kt += (bx - (vx - bx)) - (dv[oo] - ev[oo]);
+        }
+        if (j >= 1) {
+          const int oo = o - 1;
+          double ax, ay, bx, by;
+          grad_at(xv, N, i, j - 1, ax, ay);
+          const double vx = ax + ev[oo], vy = ay + ev[npix + oo];
+          shrink2(vx, vy, tau, kind, bx, by);
+          kt += (by - (vy - by)) - (dv[npix + oo] - ev[npix + oo]);
+        }
+        const double rn = r[vo + o] + mu * kt;
+        r[vo + o] = rn;
+        rrp[u] += rn * rn;
+        sv[u] = (T)rn;
+      } else {
+        sv[u] = (T)xv[o];
       }
-      if (j >= 1) {
-        const int oo = o - 1;
-        double ax, ay, bx, by;
-        grad_at(xv, N, i, j - 1, ax, ay);
-        const double vx = ax + ev[oo], vy = ay + ev[npix + oo];
-        shrink2(vx, vy, tau, kind, bx, by);
-        kt += (by - (vy - by)) - (dv[npix + oo] - ev[npix + oo]);
-      }
-      const double rn = r[vo + o] + mu * kt;
-      r[vo + o] = rn;
-      rrp += rn * rn;
-      s = (T)rn;
-    } else {
-      s = (T)xv[o];
     }
-    p[vo + o] = s;
-    tl[rw][tx] = s;
+    gstore<T, VB>(p + sbase + (size_t)o * VB, sv);
+    tile_put<T, VB>(tl, rw, tx, sv);
   }
-  tile_store_T<T>(tl, pT + vo, N, i0, j0);
+  tile_store_T<T, VB>(tl, pT + sbase, N, i0, j0);
   if (!LAST) {
-    double a[1] = {rrp};
-    block_reduce<1>(a, lds);
-    if (threadIdx.x == 0) part[(size_t)v * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + blockIdx.x] = a[0];
+    block_reduce<VB>(rrp, lds);
+    if (threadIdx.x == 0) {
+      const int P = gridDim.x * gridDim.y;
+      const int b = blockIdx.y * gridDim.x + blockIdx.x;
+#pragma unroll
+      for (int u = 0; u < VB; ++u)
+        if (u < nv) part[(size_t)(v0 + u) * P + b] = rrp[u];
+    }
   }
+}
+
+// node-major [V][L] samples -> interleaved [C][L][VB]  (grid.y = chunk)
+template <typename T, int VB>
+__global__ void k_pack(const T* __restrict__ in, T* __restrict__ out, int L, int V) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  const int chunk = blockIdx.y, v0 = chunk * VB;
+  if (q >= L) return;
+  T s[VB];
+#pragma unroll
+  for (int u = 0; u < VB; ++u) s[u] = (v0 + u < V) ? in[(size_t)(v0 + u) * L + q] : T(0);
+  gstore<T, VB>(out + ((size_t)chunk * L + q) * VB, s);
 }
 
 // ===========================================================================
@@ -706,7 +832,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce_rows(const double* __restrict
   if (threadIdx.x == 0) out[(size_t)(r / G) * ostride + ooff + (r % G)] = a[0];
 }
 
-// K x and K^T p for the operator API (float64)
+// K x and K^T p for the operator API (float64 node-major)
 __global__ void k_tv_grad(const double* __restrict__ x, double* __restrict__ gx, double* __restrict__ gy, int N) {
   const int v = blockIdx.z;
   const size_t vo = (size_t)v * N * N;

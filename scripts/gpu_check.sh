@@ -4,7 +4,7 @@
 set -u
 mkdir -p gpurun_out
 TAG=${1:-r1}
-timeout -k 10 1200 python -m pytest tests -m gpu -q -x -rA > gpurun_out/pytest_$TAG.log 2>&1
+timeout -k 10 1200 python -m pytest tests -m gpu -q -rA > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?
 echo "pytest rc=$rc"
 tail -30 gpurun_out/pytest_$TAG.log
