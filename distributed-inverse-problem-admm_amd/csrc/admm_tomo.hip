@@ -76,8 +76,8 @@ struct admm_ctx {
   admm_batch b{};
   int vb = 1;  // node interleave width of the sample buffers
   Buf xs, xsT, p, pT, Hp, sino, bI, r, c, d2, e2;
-  Buf partH, partRR, partS, partD, partE;
-  Buf redH, rrslot;
+  Buf partH, partS, partD, partE;
+  Buf redH;
   int P_back = 0, P_tile = 0, P_fwd = 0, P_edge = 0;
   hipGraph_t g_update = nullptr, g_cons = nullptr;
   hipGraphExec_t x_update = nullptr, x_cons = nullptr;
@@ -161,9 +161,8 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
   double* r = (double*)C->r.p;
   double* c = (double*)C->c.p;
   double* redH = (double*)C->redH.p;
-  double* rrslot = (double*)C->rrslot.p;
   const dim3 tg = tile_grid(C, nch);
-  const int Pt = C->P_tile, Pb = C->P_back;
+  const int Pb = C->P_back;
 
   // 1. neighbour gather: c = sum_j q_ij (z_ij - y_ij,i); xs = (T) x (+ transpose)
   hipLaunchKernelGGL((k_gather<T, VB>), tg, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.q, B.inc_off, B.inc_edge,
@@ -176,7 +175,6 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
     a.sino = sino;
     a.out_t = p;
     a.out_d = r;
-    a.part = (double*)C->partRR.p;
     a.pin = xs;
     a.dsum = B.dsum;
     a.atb = B.atb;
@@ -188,7 +186,6 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
     a.mu = B.mu;
     RET((launch_back<T, VB, BACK_INIT>(C, a, V, s)));
   }
-  RET(launch_reduce((double*)C->partRR.p, V, Pb, rrslot, 1, 1, 0, s));
   hipLaunchKernelGGL((k_transpose<T, VB>), tg, dim3(kBlock), 0, s, p, pT, N);
   CHECK_LAUNCH();
 
@@ -200,7 +197,6 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
   const int K = B.cg_iters, Tt = B.tv_iters;
   for (int t = 0; t < Tt; ++t) {
     for (int kk = 0; kk < K; ++kk) {
-      const int it = t * K + kk;
       RET((launch_fwd<T, VB, 0>(C, p, pT, sino, nullptr, nullptr, V, s)));
       BackArgs<T> a{};
       a.sino = sino;
@@ -213,20 +209,18 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
       a.lam = B.lam;
       a.mu = B.mu;
       RET((launch_back<T, VB, BACK_H>(C, a, V, s)));
-      RET(launch_reduce((double*)C->partH.p, 3 * V, Pb, redH, 1, 1, 0, s));
-      hipLaunchKernelGGL((k_cg_update<T, VB>), tg, dim3(kBlock), 0, s, B.x_ext, r, p, pT, Hp, redH,
-                         rrslot + (size_t)it * V, rrslot + (size_t)(it + 1) * V, N, V);
+      RET(launch_reduce((double*)C->partH.p, 5 * V, Pb, redH, 1, 1, 0, s));
+      hipLaunchKernelGGL((k_cg_update<T, VB>), tg, dim3(kBlock), 0, s, B.x_ext, r, p, pT, Hp, redH, N, V);
       CHECK_LAUNCH();
     }
     const bool last = (t + 1 == Tt);
     if (!last) {
       hipLaunchKernelGGL((k_tv_update<T, VB, false>), tg, dim3(kBlock), 0, s, B.x_ext, dcur, ecur, dnxt, enxt, r,
-                         p, pT, (double*)C->partRR.p, tau, B.mu, B.tv_kind, N, V);
+                         p, pT, tau, B.mu, B.tv_kind, N, V);
       CHECK_LAUNCH();
-      RET(launch_reduce((double*)C->partRR.p, V, Pt, rrslot + (size_t)(t + 1) * K * V, 1, 1, 0, s));
     } else {
       hipLaunchKernelGGL((k_tv_update<T, VB, true>), tg, dim3(kBlock), 0, s, B.x_ext, dcur, ecur, dnxt, enxt, r,
-                         xs, xsT, (double*)nullptr, tau, B.mu, B.tv_kind, N, V);
+                         xs, xsT, tau, B.mu, B.tv_kind, N, V);
       CHECK_LAUNCH();
     }
     std::swap(dcur, dnxt);
@@ -385,7 +379,7 @@ int admm_ctx_destroy(admm_ctx* C) {
   (void)hipDeviceSynchronize();
   free_graphs(C);
   Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->bI, &C->r, &C->c,
-                 &C->d2, &C->e2, &C->partH, &C->partRR, &C->partS, &C->partD, &C->partE, &C->redH, &C->rrslot};
+                 &C->d2, &C->e2, &C->partH, &C->partS, &C->partD, &C->partE, &C->redH};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (C->fang) (void)hipFree(C->fang);
@@ -507,13 +501,11 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
     return fail(ADMM_E_INVALID, "batch too large for 32-bit buffer offsets");
   C->P_fwd = ((C->g.n_det + kFwdRays - 1) / kFwdRays) * C->g.n_angles;
   C->P_edge = (int)((npix + kBlock * 4 - 1) / (kBlock * 4));
-  RET(ensure(C->partH, (size_t)3 * V * C->P_back * 8));
-  RET(ensure(C->partRR, (size_t)V * std::max(C->P_back, C->P_tile) * 8));
+  RET(ensure(C->partH, (size_t)5 * V * C->P_back * 8));
   RET(ensure(C->partS, (size_t)V * C->P_fwd * 8));
   RET(ensure(C->partD, (size_t)4 * V * C->P_back * 8));
   RET(ensure(C->partE, (size_t)3 * std::max(1, B.n_edges) * C->P_edge * 8));
-  RET(ensure(C->redH, (size_t)3 * V * 8));
-  RET(ensure(C->rrslot, (size_t)(B.tv_iters * B.cg_iters + 1) * V * 8));
+  RET(ensure(C->redH, (size_t)5 * V * 8));
   C->bound = true;
   if (C->use_graph) {
     auto fu = [&](hipStream_t s) {

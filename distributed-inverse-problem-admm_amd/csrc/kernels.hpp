@@ -126,6 +126,70 @@ __device__ __forceinline__ void block_reduce(double (&v)[NQ], double* lds /* >= 
   __syncthreads();
 }
 
+// ---------------------------------------------------------------------------
+// deterministic block reduction of NV (multiple of 16) float64 values per thread
+// by a wave-level reduce-scatter butterfly: at offsets 32, 16, 8, 4 every lane
+// keeps half of its values and adds its partner's copy of that half (NV/2 + NV/4
+// + NV/8 + NV/16 shuffles instead of 6*NV), then a plain butterfly over offsets
+// 2, 1 on the last NV/16.  Lanes with (lane & 3) == 0 then hold the wave totals;
+// the 4 waves are combined in LDS in fixed order.  On return thread t < NV of the
+// block can read total t from out_lds[t].  Fixed order -> bitwise reproducible.
+// ---------------------------------------------------------------------------
+template <int NV>
+__device__ __forceinline__ void block_reduce_rs(double (&v)[NV], double* lds /* >= 4*NV */,
+                                                double* out_lds /* >= NV */) {
+  static_assert(NV % 16 == 0, "NV must be a multiple of 16");
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV / 2; ++k) {
+    const bool hi = lane & 32;
+    const double send = hi ? v[k] : v[NV / 2 + k];
+    const double keep = hi ? v[NV / 2 + k] : v[k];
+    v[k] = keep + __shfl_xor(send, 32, 64);
+  }
+#pragma unroll
+  for (int k = 0; k < NV / 4; ++k) {
+    const bool hi = lane & 16;
+    const double send = hi ? v[k] : v[NV / 4 + k];
+    const double keep = hi ? v[NV / 4 + k] : v[k];
+    v[k] = keep + __shfl_xor(send, 16, 64);
+  }
+#pragma unroll
+  for (int k = 0; k < NV / 8; ++k) {
+    const bool hi = lane & 8;
+    const double send = hi ? v[k] : v[NV / 8 + k];
+    const double keep = hi ? v[NV / 8 + k] : v[k];
+    v[k] = keep + __shfl_xor(send, 8, 64);
+  }
+#pragma unroll
+  for (int k = 0; k < NV / 16; ++k) {
+    const bool hi = lane & 4;
+    const double send = hi ? v[k] : v[NV / 16 + k];
+    const double keep = hi ? v[NV / 16 + k] : v[k];
+    v[k] = keep + __shfl_xor(send, 4, 64);
+  }
+#pragma unroll
+  for (int k = 0; k < NV / 16; ++k) {
+    double s = v[k];
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 1, 64);
+    v[k] = s;
+  }
+  if ((lane & 3) == 0) {
+    const int base = ((lane >> 5) & 1) * (NV / 2) + ((lane >> 4) & 1) * (NV / 4) + ((lane >> 3) & 1) * (NV / 8) +
+                     ((lane >> 2) & 1) * (NV / 16);
+#pragma unroll
+    for (int k = 0; k < NV / 16; ++k) lds[wid * NV + base + k] = v[k];
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < NV) {
+    const int t = threadIdx.x;
+    out_lds[t] = (lds[t] + lds[NV + t]) + (lds[2 * NV + t] + lds[3 * NV + t]);
+  }
+  __syncthreads();
+}
+
 // ===========================================================================
 // Forward projector (Joseph, ray-driven):  sino[v][t][k] = sum_m L * interp(img_v, row m, l(m))
 // Replaces the ODL RayTransform `Ai @ x` (block_2_load_odl_data.py:72, dense form :86-114;
@@ -245,8 +309,8 @@ __global__ __launch_bounds__(kBlock) void k_fwd(const T* __restrict__ img, const
 //   BACK_PLAIN : out = A^T s  (interleaved samples)                  (operator API)
 //   BACK_ATB   : atb = A^T b (float64 node-major)                    (setup)
 //   BACK_WSQ   : W = max(sum_r A[r,p]^2, 1e-12) (float64)            (make_precisions, block_3:20-23)
-//   BACK_H     : Hp = A^T A p + rho D p + mu K^T K p; partials p.Hp, r.Hp, Hp.Hp      (CG)
-//   BACK_INIT  : r = A^T b + rho c + mu K^T(d-e) - H xs;  p = r; partial r.r         (CG start)
+//   BACK_H     : Hp = A^T A p + rho D p + mu K^T K p; partials p.Hp, r.Hp, Hp.Hp, r.r, r.p (CG)
+//   BACK_INIT  : r = A^T b + rho c + mu K^T(d-e) - H xs;  p = r                      (CG start)
 //   BACK_DIAG  : g = A^T s + rho (D x - c) + lam K^T sub(Kx); partials |g|^2, TV(x),
 //                sum_j rho/2 q_ij (x - v_ij)^2, |x - phantom|^2   (block_6_ver2.py:135-149)
 // ===========================================================================
@@ -260,7 +324,7 @@ struct BackArgs {
   // outputs
   T* out_t;                 // PLAIN: A^T s;  H: Hp;  INIT: p   (interleaved)
   double* out_d;            // ATB: atb;  WSQ: W;  INIT: r     (float64 node-major)
-  double* part;             // [V][NQ][P]
+  double* part;             // [V][NQ][P]  (NQ = 5 for H, 4 for DIAG)
   // epilogue inputs
   const T* pin;             // H: p;  INIT: xs (interleaved)
   const double* r;          // H: r
@@ -321,7 +385,7 @@ __device__ __forceinline__ double kt_w_at(const double* __restrict__ d, const do
 
 template <typename T, int VB, int MODE>
 __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
-  constexpr int NQ = (MODE == BACK_H) ? 3 : (MODE == BACK_DIAG) ? 4 : 1;
+  constexpr int NQ = (MODE == BACK_H) ? 5 : (MODE == BACK_DIAG) ? 4 : 1;
   const int N = A.N, n_det = A.n_det, n_ang = A.n_ang;
   const int npix = N * N;
   const int m_rays = n_ang * n_det;
@@ -445,16 +509,18 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
             const T hp = (T)h;
             outv[u] = hp;
             const double hd = (double)hp;
+            const double rv = A.r[vo + pix];
             pq[u][0] = pcd * hd;
-            pq[u][1] = A.r[vo + pix] * hd;
+            pq[u][1] = rv * hd;
             pq[u][2] = hd * hd;
+            pq[u][3] = rv * rv;
+            pq[u][4] = rv * pcd;
           } else {
             const double* dv = A.dvar + 2 * vo;
             const double* ev = A.evar + 2 * vo;
             const double rr = A.atb[vo + pix] + A.rho * A.cvec[vo + pix] + A.mu * kt_w_at(dv, ev, N, i, j) - h;
             A.out_d[vo + pix] = rr;
             outv[u] = (T)rr;
-            pq[u][0] = rr * rr;
           }
         }
       }
@@ -505,21 +571,24 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
       }
     }
   }
-  __shared__ double lds[4 * VB * NQ];
-  double flat[VB * NQ];
+  if constexpr (MODE == BACK_H || MODE == BACK_DIAG) {
+    constexpr int NV = ((VB * NQ + 15) / 16) * 16;
+    __shared__ double lds[4 * NV];
+    __shared__ double tot[NV];
+    double flat[NV];
 #pragma unroll
-  for (int u = 0; u < VB; ++u)
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) flat[u * NQ + q] = pq[u][q];
-  block_reduce<VB * NQ>(flat, lds);
-  if (threadIdx.x == 0) {
-    const int P = gridDim.x * gridDim.y;
-    const int b = blockIdx.y * gridDim.x + blockIdx.x;
+    for (int k = 0; k < NV; ++k) flat[k] = 0.0;
 #pragma unroll
     for (int u = 0; u < VB; ++u)
-      if (u < nv)
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) A.part[((size_t)(v0 + u) * NQ + q) * P + b] = flat[u * NQ + q];
+      for (int q = 0; q < NQ; ++q) flat[u * NQ + q] = pq[u][q];
+    block_reduce_rs<NV>(flat, lds, tot);
+    const int t = threadIdx.x;
+    if (t < VB * NQ && t / NQ < nv) {
+      const int P = gridDim.x * gridDim.y;
+      const int b = blockIdx.y * gridDim.x + blockIdx.x;
+      A.part[((size_t)v0 * NQ + t) * P + b] = tot[t];
+    }
   }
 }
 
@@ -606,14 +675,13 @@ __global__ __launch_bounds__(kBlock) void k_transpose(const T* __restrict__ in, 
   tile_store_T<T, VB>(tl, outT + sbase, N, i0, j0);
 }
 
-// CG step with the single-reduction identity (oracle/node_solver.py):
-//   alpha = rr/pHp, rr' = rr - 2 alpha rHp + alpha^2 HpHp, beta = rr'/rr
+// CG step from the five reductions of the preceding BACK_H launch (oracle/node_solver.py):
+//   alpha = r.p / p.Hp (exact line search),  rr' = rr - 2 alpha rHp + alpha^2 HpHp,  beta = rr'/rr
 //   x += alpha p;  r -= alpha Hp;  p = r + beta p  (p also written transposed)
 template <typename T, int VB>
 __global__ __launch_bounds__(kBlock) void k_cg_update(double* __restrict__ x, double* __restrict__ r,
                                                       T* __restrict__ p, T* __restrict__ pT,
                                                       const T* __restrict__ Hp, const double* __restrict__ redH,
-                                                      const double* __restrict__ rr_in, double* __restrict__ rr_out,
                                                       int N, int V) {
   __shared__ TileT<T, VB> tl;
   const int chunk = blockIdx.z, v0 = chunk * VB, nv = min(VB, V - v0);
@@ -626,14 +694,13 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(double* __restrict__ x, do
     beta[u] = 0.0;
     if (u < nv) {
       const int v = v0 + u;
-      const double pHp = redH[3 * v + 0], rHp = redH[3 * v + 1], HH = redH[3 * v + 2];
-      const double rr = rr_in[v];
-      const double al = (pHp != 0.0) ? rr / pHp : 0.0;
+      const double* S = redH + 5 * v;
+      const double pHp = S[0], rHp = S[1], HH = S[2], rr = S[3], rp = S[4];
+      const double al = (pHp != 0.0) ? rp / pHp : 0.0;
       double rrn = rr - 2.0 * al * rHp + al * al * HH;
       rrn = fmax(rrn, 0.0);
       alpha[u] = al;
       beta[u] = (rr != 0.0) ? rrn / rr : 0.0;
-      if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) rr_out[v] = rrn;
     }
   }
   const int i0 = blockIdx.y * kTile, j0 = blockIdx.x * kTile;
@@ -666,8 +733,8 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(double* __restrict__ x, do
 
 // split-Bregman (d, e) update after a CG solve:
 //   u = Kx + e, d' = shrink(u, lam/mu), e' = u - d'
-// and, unless LAST, the residual shift r += mu K^T((d'-e') - (d-e)), restart p = r,
-// partial r.r.  With LAST the sample copy xs = (T) x (+ transpose) is produced for
+// and, unless LAST, the residual shift r += mu K^T((d'-e') - (d-e)) and the CG
+// restart p = r.  With LAST the sample copy xs = (T) x (+ transpose) is produced for
 // the diagnostics epilogue instead.  d/e are ping-ponged (din -> dout) because the
 // stencil reads neighbours' old values.
 __device__ __forceinline__ void shrink2(double ux, double uy, double tau, int kind, double& dx, double& dy) {
@@ -686,19 +753,14 @@ template <typename T, int VB, bool LAST>
 __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__ x, const double* __restrict__ din,
                                                       const double* __restrict__ ein, double* __restrict__ dout,
                                                       double* __restrict__ eout, double* __restrict__ r,
-                                                      T* __restrict__ p, T* __restrict__ pT,
-                                                      double* __restrict__ part, double tau, double mu, int kind,
-                                                      int N, int V) {
+                                                      T* __restrict__ p, T* __restrict__ pT, double tau,
+                                                      double mu, int kind, int N, int V) {
   __shared__ TileT<T, VB> tl;
-  __shared__ double lds[4 * VB];
   const int chunk = blockIdx.z, v0 = chunk * VB, nv = min(VB, V - v0);
   const int npix = N * N;
   const size_t sbase = (size_t)chunk * npix * VB;
   const int i0 = blockIdx.y * kTile, j0 = blockIdx.x * kTile;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  double rrp[VB];
-#pragma unroll
-  for (int u = 0; u < VB; ++u) rrp[u] = 0.0;
   for (int rw = ty; rw < kTile; rw += 8) {
     const int i = i0 + rw, j = j0 + tx;
     if (i >= N || j >= N) continue;
@@ -745,7 +807,6 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
         }
         const double rn = r[vo + o] + mu * kt;
         r[vo + o] = rn;
-        rrp[u] += rn * rn;
         sv[u] = (T)rn;
       } else {
         sv[u] = (T)xv[o];
@@ -755,16 +816,6 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
     tile_put<T, VB>(tl, rw, tx, sv);
   }
   tile_store_T<T, VB>(tl, pT + sbase, N, i0, j0);
-  if (!LAST) {
-    block_reduce<VB>(rrp, lds);
-    if (threadIdx.x == 0) {
-      const int P = gridDim.x * gridDim.y;
-      const int b = blockIdx.y * gridDim.x + blockIdx.x;
-#pragma unroll
-      for (int u = 0; u < VB; ++u)
-        if (u < nv) part[(size_t)(v0 + u) * P + b] = rrp[u];
-    }
-  }
 }
 
 // node-major [V][L] samples -> interleaved [C][L][VB]  (grid.y = chunk)

@@ -182,6 +182,11 @@ SHEPP_LOGAN_MODIFIED = np.array(
 
 def shepp_logan(N: int, supersample: int = 1) -> np.ndarray:
     """Modified Shepp-Logan on [-1,1]^2, array[i, j] <-> (x_i, y_j)."""
+    return ellipse_phantom(N, SHEPP_LOGAN_MODIFIED, supersample)
+
+
+def ellipse_phantom(N: int, table, supersample: int = 1) -> np.ndarray:
+    """Sum of ellipses [value, a, b, x0, y0, phi_deg] on [-1,1]^2, pixel-averaged."""
     h = 2.0 / N
     ss = supersample
     sub = (np.arange(ss) + 0.5) / ss - 0.5
@@ -189,7 +194,7 @@ def shepp_logan(N: int, supersample: int = 1) -> np.ndarray:
     X = (xc[:, None] + sub[None, :] * h).ravel()
     XX, YY = np.meshgrid(X, X, indexing="ij")
     img = np.zeros_like(XX)
-    for v, a, b, x0, y0, phi in SHEPP_LOGAN_MODIFIED:
+    for v, a, b, x0, y0, phi in table:
         p = math.radians(phi)
         xr = (XX - x0) * math.cos(p) + (YY - y0) * math.sin(p)
         yr = -(XX - x0) * math.sin(p) + (YY - y0) * math.cos(p)
@@ -200,10 +205,15 @@ def shepp_logan(N: int, supersample: int = 1) -> np.ndarray:
 
 def shepp_logan_radon(geom: Geometry) -> np.ndarray:
     """Analytic line integrals of :func:`shepp_logan` for ``geom`` (a, n_det)."""
+    return ellipse_radon(geom, SHEPP_LOGAN_MODIFIED)
+
+
+def ellipse_radon(geom: Geometry, table) -> np.ndarray:
+    """Analytic line integrals over the lines x cos(t) + y sin(t) = s (a, n_det)."""
     th = geom.angles[:, None]
     s = geom.det_centers[None, :]
     out = np.zeros((geom.n_angles, geom.n_det))
-    for v, a, b, x0, y0, phi in SHEPP_LOGAN_MODIFIED:
+    for v, a, b, x0, y0, phi in table:
         p = math.radians(phi)
         sp_ = s - (x0 * np.cos(th) + y0 * np.sin(th))
         d2 = (a * np.cos(th - p)) ** 2 + (b * np.sin(th - p)) ** 2

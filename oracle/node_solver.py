@@ -14,9 +14,13 @@ build replaces it with a deterministic fixed-count split-Bregman iteration
 
 solved by ``cg_iters`` conjugate-gradient steps warm-started from the current
 x.  The CG keeps its residual recursively across TV rounds
-(r += mu K^T (w_new - w_old), w = d - e) and uses the single-reduction
-identity ||r - a Hp||^2 = rr - 2a r.Hp + a^2 Hp.Hp, exactly as the HIP path
-(csrc/admm_kernels.hip) does.  Scalars are float64; vectors are float64 by
+(r += mu K^T (w_new - w_old), w = d - e) and takes every scalar from ONE fused
+reduction per step (the back-projector epilogue on the device):
+p.Hp, r.Hp, Hp.Hp, r.r, r.p.  The step is the exact line search
+alpha = r.p / p.Hp (equal to r.r / p.Hp in exact CG, but stable when
+orthogonality is lost), and beta = ||r - alpha Hp||^2 / r.r with the numerator
+from the identity rr - 2 alpha r.Hp + alpha^2 Hp.Hp -- exactly as the HIP path
+(csrc/kernels.hpp k_back<BACK_H>, k_cg_update) does.  Scalars are float64; vectors are float64 by
 default or float32 (``dtype``) to emulate the device arithmetic.
 """
 from __future__ import annotations
@@ -88,7 +92,6 @@ def node_update(A, Atb, b, D, c, qv_terms, st: NodeState, N: int, p: NodeParams,
     wy = cast(st.dy - st.ey)
     r = cast(Atb + rho * c + mu * tvmod.div_t(wx, wy, N) - H(x))
     pvec = r.copy()
-    rr = _dot(r, r)
     diag = NodeDiag()
     for t in range(p.tv_iters):
         for _ in range(p.cg_iters):
@@ -96,14 +99,15 @@ def node_update(A, Atb, b, D, c, qv_terms, st: NodeState, N: int, p: NodeParams,
             pHp = _dot(pvec, Hp)
             rHp = _dot(r, Hp)
             HpHp = _dot(Hp, Hp)
-            alpha = rr / pHp if pHp != 0.0 else 0.0
+            rr = _dot(r, r)
+            rp = _dot(r, pvec)
+            alpha = rp / pHp if pHp != 0.0 else 0.0
             rr_new = rr - 2.0 * alpha * rHp + alpha * alpha * HpHp
             rr_new = max(rr_new, 0.0)
             beta = rr_new / rr if rr != 0.0 else 0.0
             x += cast(alpha * pvec)
             r -= cast(alpha * Hp)
             pvec = cast(r + beta * pvec)
-            rr = rr_new
             diag.cg_rr.append(rr)
         # TV (d, e) update: u = Kx + e, d = shrink(u, lam/mu), e = u - d
         gx, gy = tvmod.grad(x, N)
@@ -120,7 +124,6 @@ def node_update(A, Atb, b, D, c, qv_terms, st: NodeState, N: int, p: NodeParams,
             r += cast(mu * tvmod.div_t(nwx - wx, nwy - wy, N))
             wx, wy = nwx, nwy
             pvec = r.copy()
-            rr = _dot(r, r)
     # Epilogue diagnostics (block_6_admm_loop_ver2.py:125-149,189-197)
     s = cast(A @ x) - cast(b)
     diag.mse_sino = _dot(s, s)
