@@ -107,7 +107,7 @@ int with_vb(int vb, F&& f) {
 template <typename T, int VB, int MODE>
 int launch_fwd(admm_ctx* C, const T* img, const T* imgT, T* sino, const T* b, double* part, int V, hipStream_t s) {
   dim3 grid((C->g.n_det + kFwdRays - 1) / kFwdRays, C->g.n_angles, (V + VB - 1) / VB);
-  hipLaunchKernelGGL((k_fwd<T, VB, MODE>), grid, dim3(kBlock), 0, s, img, imgT, sino, b, part, C->fang, C->g.N,
+  hipLaunchKernelGGL((k_fwd<T, VB, MODE>), grid, dim3(kFwdBlock), 0, s, img, imgT, sino, b, part, C->fang, C->g.N,
                      C->g.n_det, C->g.n_angles, V);
   CHECK_LAUNCH();
   return ADMM_OK;
@@ -121,8 +121,7 @@ int launch_back(admm_ctx* C, BackArgs<T> a, int V, hipStream_t s) {
   a.n_ang = C->g.n_angles;
   a.V = V;
   const int N = C->g.N;
-  dim3 grid((N + kBackTileJ - 1) / kBackTileJ, (N + kBackTileI - 1) / kBackTileI,
-            MODE == BACK_WSQ ? 1 : (V + VB - 1) / VB);
+  dim3 grid((N + kBTJ - 1) / kBTJ, (N + kBTI - 1) / kBTI, MODE == BACK_WSQ ? 1 : (V + VB - 1) / VB);
   hipLaunchKernelGGL((k_back<T, VB, MODE>), grid, dim3(kBlock), 0, s, a);
   CHECK_LAUNCH();
   return ADMM_OK;
@@ -130,11 +129,11 @@ int launch_back(admm_ctx* C, BackArgs<T> a, int V, hipStream_t s) {
 
 int back_partitions(admm_ctx* C) {
   const int N = C->g.N;
-  return ((N + kBackTileJ - 1) / kBackTileJ) * ((N + kBackTileI - 1) / kBackTileI);
+  return ((N + kBTJ - 1) / kBTJ) * ((N + kBTI - 1) / kBTI);
 }
-dim3 tile_grid(admm_ctx* C, int nchunks) {
-  const int N = C->g.N;
-  return dim3((N + kTile - 1) / kTile, (N + kTile - 1) / kTile, nchunks);
+dim3 tile_grid(admm_ctx* C, int nchunks, int vb) {
+  const int N = C->g.N, ti = kTile / vb;
+  return dim3((N + kTile - 1) / kTile, (N + ti - 1) / ti, nchunks);
 }
 
 int launch_reduce(const double* part, int rows, int P, double* out, int G, int ostride, int ooff, hipStream_t s) {
@@ -161,7 +160,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
   double* r = (double*)C->r.p;
   double* c = (double*)C->c.p;
   double* redH = (double*)C->redH.p;
-  const dim3 tg = tile_grid(C, nch);
+  const dim3 tg = tile_grid(C, nch, VB);
   const int Pb = C->P_back;
 
   // 1. neighbour gather: c = sum_j q_ij (z_ij - y_ij,i); xs = (T) x (+ transpose)
@@ -395,7 +394,7 @@ int admm_project_fwd(admm_ctx* C, const void* img, void* sino, int nimg, void* s
   hipStream_t s = (hipStream_t)stream;
   const size_t ds = dsize(C->dtype);
   RET(ensure(C->op_imgT, (size_t)nimg * C->npix * ds));
-  const dim3 tg = tile_grid(C, nimg);
+  const dim3 tg = tile_grid(C, nimg, 1);
   // operator API: node-major images = interleave width 1
   if (C->dtype == ADMM_DTYPE_F32) {
     hipLaunchKernelGGL((k_transpose<float, 1>), tg, dim3(kBlock), 0, s, (const float*)img, (float*)C->op_imgT.p,

@@ -29,11 +29,9 @@ namespace admm {
 
 constexpr int kBlock = 256;
 constexpr int kTile = 32;        // elementwise / transposing kernels: 32x32 pixel tiles, block 32 x 8
-constexpr int kBackTileJ = 64;   // back-projector block: 64 (j) x 4 (i) pixels
-constexpr int kBackTileI = 4;
-constexpr int kFwdRays = 64;     // forward-projector block: 64 rays x 4 step segments
-constexpr int kFwdSegs = 4;
-constexpr int kAngChunk = 256;   // back-projector angle table chunk staged in LDS
+constexpr int kFwdRays = 64;     // forward-projector block: 64 rays x 8 step segments (512 threads)
+constexpr int kFwdSegs = 8;
+constexpr int kFwdBlock = kFwdRays * kFwdSegs;
 
 // Per-angle forward-projector constants (host-computed in float64).
 // Ray (t,k), step m:  l = A0 + k*A1 + m*dl  (interpolation coordinate).
@@ -195,16 +193,16 @@ __device__ __forceinline__ void block_reduce_rs(double (&v)[NV], double* lds /* 
 // Replaces the ODL RayTransform `Ai @ x` (block_2_load_odl_data.py:72, dense form :86-114;
 // used at block_5_node_problem.py:21 and block_6_admm_loop_ver2.py:193).
 //
-// Block = 64 consecutive detector bins of one angle x 4 step segments (one wave each).
+// Block = 64 consecutive detector bins of one angle x 8 step segments (one wave each).
 // Lanes are consecutive rays, so at every step a wave reads one contiguous row segment:
 // case-B angles read img (row m = axis-0 index), case-A angles read the transposed
 // copy imgT (row m = axis-1 index).  Each tap is one VB-vector load (VB nodes).
-// The 4 segment partial sums are combined in LDS in fixed order.
+// The 8 segment partial sums are combined in LDS in fixed order.
 // MODE 0: store A x (interleaved).
 // MODE 1: store s = A x - b (interleaved; b node-major [V][m]) and partials of ||s||^2.
 // ===========================================================================
 template <typename T, int VB, int MODE>
-__global__ __launch_bounds__(kBlock) void k_fwd(const T* __restrict__ img, const T* __restrict__ imgT,
+__global__ __launch_bounds__(kFwdBlock) void k_fwd(const T* __restrict__ img, const T* __restrict__ imgT,
                                                 T* __restrict__ sino, const T* __restrict__ bsino,
                                                 double* __restrict__ part, const FwdAngle* __restrict__ ang,
                                                 int N, int n_det, int n_ang, int V) {
@@ -241,24 +239,41 @@ __global__ __launch_bounds__(kBlock) void k_fwd(const T* __restrict__ img, const
     const int segLen = (N + kFwdSegs - 1) / kFwdSegs;
     const int s0 = max(mlo, seg * segLen);
     const int s1 = min(mhi, seg * segLen + segLen - 1);
-    for (int m = s0; m <= s1; ++m) {
+    // two steps per iteration: both steps' loads are in flight before the FMAs
+    auto tap = [&](int m, T (&p0)[VB], T (&p1)[VB], T& w0, T& w1) {
       const double l = fma((double)m, a.dl, l0);
       const double fl = floor(l);
       const int i0 = (int)fl;
-      T w1 = (T)(l - fl);
-      T w0 = T(1) - w1;
+      w1 = (T)(l - fl);
+      w0 = T(1) - w1;
       w0 = (i0 >= 0 && i0 <= N - 1) ? w0 : T(0);
       w1 = (i0 >= -1 && i0 <= N - 2) ? w1 : T(0);
       const int row = m * N;
       const int o0 = (row + clampi(i0, 0, N - 1)) * VB * (int)sizeof(T);
       const int o1 = (row + clampi(i0 + 1, 0, N - 1)) * VB * (int)sizeof(T);
-      T p0[VB], p1[VB];
       vload<T, VB>(rs, o0, soff, p0);
       vload<T, VB>(rs, o1, soff, p1);
+    };
+    int m = s0;
+    for (; m + 1 <= s1; m += 2) {
+      T a0[VB], a1[VB], b0[VB], b1[VB], wa0, wa1, wb0, wb1;
+      tap(m, a0, a1, wa0, wa1);
+      tap(m + 1, b0, b1, wb0, wb1);
 #pragma unroll
       for (int u = 0; u < VB; ++u) {
-        acc[u] = fma(w0, p0[u], acc[u]);
-        acc[u] = fma(w1, p1[u], acc[u]);
+        acc[u] = fma(wa0, a0[u], acc[u]);
+        acc[u] = fma(wa1, a1[u], acc[u]);
+        acc[u] = fma(wb0, b0[u], acc[u]);
+        acc[u] = fma(wb1, b1[u], acc[u]);
+      }
+    }
+    if (m <= s1) {
+      T a0[VB], a1[VB], wa0, wa1;
+      tap(m, a0, a1, wa0, wa1);
+#pragma unroll
+      for (int u = 0; u < VB; ++u) {
+        acc[u] = fma(wa0, a0[u], acc[u]);
+        acc[u] = fma(wa1, a1[u], acc[u]);
       }
     }
   }
@@ -274,7 +289,9 @@ __global__ __launch_bounds__(kBlock) void k_fwd(const T* __restrict__ img, const
     T s[VB];
 #pragma unroll
     for (int u = 0; u < VB; ++u) {
-      s[u] = ((red[0][u][lane] + red[1][u][lane]) + (red[2][u][lane] + red[3][u][lane])) * (T)a.L;
+      s[u] = (((red[0][u][lane] + red[1][u][lane]) + (red[2][u][lane] + red[3][u][lane])) +
+              ((red[4][u][lane] + red[5][u][lane]) + (red[6][u][lane] + red[7][u][lane]))) *
+             (T)a.L;
       if (MODE == 1) {
         if (u < nv) {
           s[u] = s[u] - bsino[(size_t)(v0 + u) * n_ang * n_det + ray];
@@ -286,11 +303,16 @@ __global__ __launch_bounds__(kBlock) void k_fwd(const T* __restrict__ img, const
     }
     gstore<T, VB>(sino + ((size_t)chunk * n_ang * n_det + ray) * VB, s);
   }
-  if (MODE == 1) {
-    __syncthreads();
-    __shared__ double lds[4 * VB];
-    block_reduce<VB>(sq, lds);
-    if (threadIdx.x == 0) {
+  if (MODE == 1 && seg == 0) {
+    // only wave 0 holds residuals: one fixed-order wave reduction per node
+#pragma unroll
+    for (int u = 0; u < VB; ++u) {
+      double v = sq[u];
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+      sq[u] = v;
+    }
+    if (lane == 0) {
       const int P = gridDim.x * gridDim.y;
       const int b = blockIdx.y * gridDim.x + blockIdx.x;
 #pragma unroll
@@ -383,83 +405,250 @@ __device__ __forceinline__ double kt_w_at(const double* __restrict__ d, const do
   return s;
 }
 
+// Fused epilogue of one pixel: writes the mode's per-pixel outputs and adds the
+// pixel's reduction terms into pq.
+template <typename T, int VB, int MODE, int NQ>
+__device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j, int chunk, int v0, int nv,
+                                              const T (&acc)[VB], double (&pq)[VB][NQ]) {
+  const int N = A.N;
+  const int npix = N * N;
+  const int pix = i * N + j;
+  const size_t sbase = (size_t)chunk * npix * VB;  // interleaved sample base of this chunk
+  if constexpr (MODE == BACK_PLAIN) {
+    gstore<T, VB>(A.out_t + sbase + (size_t)pix * VB, acc);
+  } else if constexpr (MODE == BACK_ATB) {
+#pragma unroll
+    for (int u = 0; u < VB; ++u)
+      if (u < nv) A.out_d[(size_t)(v0 + u) * npix + pix] = (double)acc[u];
+  } else if constexpr (MODE == BACK_WSQ) {
+    A.out_d[pix] = fmax((double)acc[0], 1e-12);
+  } else if constexpr (MODE == BACK_H || MODE == BACK_INIT) {
+    // H v = acc + rho D v + mu K^T K v  (v = p or xs, interleaved samples)
+    const T* pv = A.pin + sbase;
+    T pc[VB], pn[VB];
+    double ktk[VB];
+    gload<T, VB>(pv + (size_t)pix * VB, pc);
+#pragma unroll
+    for (int u = 0; u < VB; ++u) ktk[u] = 0.0;
+    if (i >= 1) {
+      gload<T, VB>(pv + (size_t)(pix - N) * VB, pn);
+#pragma unroll
+      for (int u = 0; u < VB; ++u) ktk[u] += (double)pc[u] - (double)pn[u];
+    }
+    if (i <= N - 2) {
+      gload<T, VB>(pv + (size_t)(pix + N) * VB, pn);
+#pragma unroll
+      for (int u = 0; u < VB; ++u) ktk[u] -= (double)pn[u] - (double)pc[u];
+    }
+    if (j >= 1) {
+      gload<T, VB>(pv + (size_t)(pix - 1) * VB, pn);
+#pragma unroll
+      for (int u = 0; u < VB; ++u) ktk[u] += (double)pc[u] - (double)pn[u];
+    }
+    if (j <= N - 2) {
+      gload<T, VB>(pv + (size_t)(pix + 1) * VB, pn);
+#pragma unroll
+      for (int u = 0; u < VB; ++u) ktk[u] -= (double)pn[u] - (double)pc[u];
+    }
+    T outv[VB];
+#pragma unroll
+    for (int u = 0; u < VB; ++u) {
+      outv[u] = T(0);
+      if (u < nv) {
+        const size_t vo = (size_t)(v0 + u) * npix;
+        const double pcd = (double)pc[u];
+        const double h = (double)acc[u] + A.rho * A.dsum[vo + pix] * pcd + A.mu * ktk[u];
+        if constexpr (MODE == BACK_H) {
+          const T hp = (T)h;
+          outv[u] = hp;
+          const double hd = (double)hp;
+          const double rv = A.r[vo + pix];
+          pq[u][0] += pcd * hd;
+          pq[u][1] += rv * hd;
+          pq[u][2] += hd * hd;
+          pq[u][3] += rv * rv;
+          pq[u][4] += rv * pcd;
+        } else {
+          const double* dv = A.dvar + 2 * vo;
+          const double* ev = A.evar + 2 * vo;
+          const double rr = A.atb[vo + pix] + A.rho * A.cvec[vo + pix] + A.mu * kt_w_at(dv, ev, N, i, j) - h;
+          A.out_d[vo + pix] = rr;
+          outv[u] = (T)rr;
+        }
+      }
+    }
+    gstore<T, VB>(A.out_t + sbase + (size_t)pix * VB, outv);
+  } else if constexpr (MODE == BACK_DIAG) {
+#pragma unroll
+    for (int u = 0; u < VB; ++u) {
+      if (u >= nv) continue;
+      const int v = v0 + u;
+      const size_t vo = (size_t)v * npix;
+      const double* xv = A.x + vo;
+      const double xc = xv[pix];
+      // lam * K^T sub(Kx) at (i,j): needs the subgradient at (i,j), (i-1,j), (i,j-1)
+      double gx, gy, px, py, kts = 0.0, tvv;
+      grad_at(xv, N, i, j, gx, gy);
+      tv_sub(gx, gy, A.tv_kind, px, py);
+      tvv = (A.tv_kind == 0) ? sqrt(gx * gx + gy * gy) : fabs(gx) + fabs(gy);
+      if (i <= N - 2) kts -= px;
+      if (j <= N - 2) kts -= py;
+      if (i >= 1) {
+        double ax, ay, bx, by;
+        grad_at(xv, N, i - 1, j, ax, ay);
+        tv_sub(ax, ay, A.tv_kind, bx, by);
+        kts += bx;
+      }
+      if (j >= 1) {
+        double ax, ay, bx, by;
+        grad_at(xv, N, i, j - 1, ax, ay);
+        tv_sub(ax, ay, A.tv_kind, bx, by);
+        kts += by;
+      }
+      const double cc = A.cvec[vo + pix];
+      const double g = (double)acc[u] + A.rho * (A.dsum[vo + pix] * xc - cc) + A.lam * kts;
+      double quad = 0.0;
+      for (int q = A.inc_off[v]; q < A.inc_off[v + 1]; ++q) {
+        const size_t eo = (size_t)A.inc_edge[q] * npix + pix;
+        const double vij = A.zv[eo] - (double)A.inc_sign[q] * A.yv[eo];
+        const double dd = xc - vij;
+        quad += A.qv[(size_t)A.inc_qslot[q] * npix + pix] * dd * dd;
+      }
+      pq[u][0] += g * g;
+      pq[u][1] += tvv;
+      pq[u][2] += 0.5 * A.rho * quad;
+      if (A.phantom) {
+        const double dp = xc - A.phantom[pix];
+        pq[u][3] += dp * dp;
+      }
+    }
+  }
+}
+
+// Back projector.  Block = 64 (j) x 4 (i) pixel tile, one pixel per thread.
+// Per chunk of kBAngC angles the block stages, for each angle, the window of
+// kBWin detector bins its tile can touch (from the floor of the smallest corner
+// k_f, minus 1) into LDS, zero-filled outside the detector, so each tap is an
+// LDS read with no bin-range predicate; every staged bin serves ~7 taps.  A
+// VB-vector of samples (32 B for 8 float nodes) is split into 16-byte planes so
+// that lanes reading consecutive bins hit consecutive banks (no conflicts).
+// Two angles are processed per iteration to keep 4 LDS reads in flight.
+constexpr int kBTJ = 64;
+constexpr int kBTI = 4;
+constexpr int kBAngC = 16;
+constexpr int kBWin = 72;
+
+template <typename T, int VB>
+struct Planes {
+  static constexpr int BYTES = VB * (int)sizeof(T);
+  static constexpr int NPL = BYTES > 16 ? BYTES / 16 : 1;  // 16-byte planes
+  static constexpr int PV = VB / NPL;                      // values per plane
+};
+
 template <typename T, int VB, int MODE>
 __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
   constexpr int NQ = (MODE == BACK_H) ? 5 : (MODE == BACK_DIAG) ? 4 : 1;
+  constexpr int NPL = Planes<T, VB>::NPL, PV = Planes<T, VB>::PV;
   const int N = A.N, n_det = A.n_det, n_ang = A.n_ang;
-  const int npix = N * N;
   const int m_rays = n_ang * n_det;
-  const int j = blockIdx.x * kBackTileJ + (threadIdx.x & 63);
-  const int i = blockIdx.y * kBackTileI + (threadIdx.x >> 6);
+  const int jb = blockIdx.x * kBTJ, ib = blockIdx.y * kBTI;
+  const int j = jb + (threadIdx.x & 63);
+  const int i = ib + (threadIdx.x >> 6);
   const bool inb = (i < N) && (j < N);
   const int chunk = blockIdx.z;
   const int v0 = chunk * VB;
   const int nv = (MODE == BACK_WSQ) ? 1 : min(VB, A.V - v0);
-  const int nch = (A.V + VB - 1) / VB;
-  const __amdgpu_buffer_rsrc_t rs =
-      make_rsrc(A.sino, (uint32_t)((size_t)nch * m_rays * VB * sizeof(T)));
-  const int soff = chunk * m_rays * VB * (int)sizeof(T);
+  // geometry uses clamped coordinates so out-of-image threads stay inside the window
+  const double djc = (double)min(j, N - 1), dic = (double)min(i, N - 1);
+  const int jhi = min(jb + kBTJ - 1, N - 1), ihi = min(ib + kBTI - 1, N - 1);
 
-  __shared__ BackAngle sang[kAngChunk];
+  __shared__ Pack<T, PV> win[NPL][(MODE == BACK_WSQ) ? 1 : kBAngC][kBWin];
+  __shared__ BackAngle sang[kBAngC];
+  __shared__ int kmin_s[kBAngC];
   T acc[VB];
 #pragma unroll
   for (int u = 0; u < VB; ++u) acc[u] = T(0);
-  const double di = (double)i, dj = (double)j;
+  const T* sino_c = A.sino + (size_t)chunk * m_rays * VB;
 
-  for (int t0 = 0; t0 < n_ang; t0 += kAngChunk) {
-    const int nt = min(kAngChunk, n_ang - t0);
-    __syncthreads();
-    for (int q = threadIdx.x; q < nt; q += kBlock) sang[q] = A.ang[t0 + q];
-    __syncthreads();
-    if (inb) {
-      for (int tt = 0; tt < nt; ++tt) {
-        const BackAngle g = sang[tt];
-        const double kf = fma(di, g.Bi, fma(dj, g.Bj, g.B0));
-        const double kfl = floor(kf);
-        const int k0 = (int)kfl;
-        const T f = (T)(kf - kfl);
-        T w0 = fmax(T(0), T(1) - f * (T)g.slope) * (T)g.L;
-        T w1 = fmax(T(0), T(1) - (T(1) - f) * (T)g.slope) * (T)g.L;
-        w0 = (k0 >= 0 && k0 <= n_det - 1) ? w0 : T(0);
-        w1 = (k0 >= -1 && k0 <= n_det - 2) ? w1 : T(0);
-        if (MODE == BACK_WSQ) {
-          acc[0] = fma(w0, w0, acc[0]);
-          acc[0] = fma(w1, w1, acc[0]);
-        } else {
-          const int rowo = (t0 + tt) * n_det;
-          const int o0 = (rowo + clampi(k0, 0, n_det - 1)) * VB * (int)sizeof(T);
-          const int o1 = (rowo + clampi(k0 + 1, 0, n_det - 1)) * VB * (int)sizeof(T);
-          T s0[VB], s1[VB];
-          vload<T, VB>(rs, o0, soff, s0);
-          vload<T, VB>(rs, o1, soff, s1);
+  auto tap = [&](int tt, T& w0, T& w1, Pack<T, PV> (&s0)[NPL], Pack<T, PV> (&s1)[NPL]) {
+    const BackAngle g = sang[tt];
+    const double kf = fma(dic, g.Bi, fma(djc, g.Bj, g.B0));
+    const double kfl = floor(kf);
+    const int k0 = (int)kfl;
+    const T f = (T)(kf - kfl);
+    w0 = fmax(T(0), T(1) - f * (T)g.slope) * (T)g.L;
+    w1 = fmax(T(0), T(1) - (T(1) - f) * (T)g.slope) * (T)g.L;
+    if constexpr (MODE == BACK_WSQ) {
+      w0 = (k0 >= 0 && k0 <= n_det - 1) ? w0 : T(0);
+      w1 = (k0 >= -1 && k0 <= n_det - 2) ? w1 : T(0);
+    } else {
+      const int idx = k0 - kmin_s[tt];
 #pragma unroll
-          for (int u = 0; u < VB; ++u) {
-            acc[u] = fma(w0, s0[u], acc[u]);
-            acc[u] = fma(w1, s1[u], acc[u]);
-          }
-        }
+      for (int q = 0; q < NPL; ++q) {
+        s0[q] = win[q][tt][idx];
+        s1[q] = win[q][tt][idx + 1];
       }
     }
-  }
-
-  // ---------------- fused epilogues ----------------
-  const int pix = i * N + j;
-  const size_t sbase = (size_t)chunk * npix * VB;  // interleaved sample base of this chunk
-  if (MODE == BACK_PLAIN) {
-    if (inb) gstore<T, VB>(A.out_t + sbase + (size_t)pix * VB, acc);
-    return;
-  }
-  if (MODE == BACK_ATB) {
-    if (inb) {
+  };
+  auto fmac = [&](T w0, T w1, const Pack<T, PV> (&s0)[NPL], const Pack<T, PV> (&s1)[NPL]) {
+    if constexpr (MODE == BACK_WSQ) {
+      acc[0] = fma(w0, w0, acc[0]);
+      acc[0] = fma(w1, w1, acc[0]);
+    } else {
 #pragma unroll
-      for (int u = 0; u < VB; ++u)
-        if (u < nv) A.out_d[(size_t)(v0 + u) * npix + pix] = (double)acc[u];
+      for (int q = 0; q < NPL; ++q)
+#pragma unroll
+        for (int e = 0; e < PV; ++e) {
+          acc[q * PV + e] = fma(w0, s0[q].v[e], acc[q * PV + e]);
+          acc[q * PV + e] = fma(w1, s1[q].v[e], acc[q * PV + e]);
+        }
     }
-    return;
-  }
-  if (MODE == BACK_WSQ) {
-    if (inb) A.out_d[pix] = fmax((double)acc[0], 1e-12);
-    return;
+  };
+
+  for (int t0 = 0; t0 < n_ang; t0 += kBAngC) {
+    const int nt = min(kBAngC, n_ang - t0);
+    __syncthreads();
+    if ((int)threadIdx.x < nt) {
+      const BackAngle g = A.ang[t0 + threadIdx.x];
+      sang[threadIdx.x] = g;
+      const double k00 = fma((double)ib, g.Bi, fma((double)jb, g.Bj, g.B0));
+      const double k01 = fma((double)ib, g.Bi, fma((double)jhi, g.Bj, g.B0));
+      const double k10 = fma((double)ihi, g.Bi, fma((double)jb, g.Bj, g.B0));
+      const double k11 = fma((double)ihi, g.Bi, fma((double)jhi, g.Bj, g.B0));
+      kmin_s[threadIdx.x] = (int)floor(fmin(fmin(k00, k01), fmin(k10, k11))) - 1;
+    }
+    __syncthreads();
+    if constexpr (MODE != BACK_WSQ) {
+      for (int q = threadIdx.x; q < nt * kBWin * NPL; q += kBlock) {
+        const int pl = q % NPL, aw = q / NPL;
+        const int a = aw / kBWin, w = aw - a * kBWin;
+        const int k = kmin_s[a] + w;
+        Pack<T, PV> val;
+        if (k >= 0 && k < n_det) {
+          val = *reinterpret_cast<const Pack<T, PV>*>(sino_c + ((size_t)(t0 + a) * n_det + k) * VB + pl * PV);
+        } else {
+#pragma unroll
+          for (int e = 0; e < PV; ++e) val.v[e] = T(0);
+        }
+        win[pl][a][w] = val;
+      }
+      __syncthreads();
+    }
+    int tt = 0;
+    for (; tt + 1 < nt; tt += 2) {
+      T wa0, wa1, wb0, wb1;
+      Pack<T, PV> sa0[NPL], sa1[NPL], sb0[NPL], sb1[NPL];
+      tap(tt, wa0, wa1, sa0, sa1);
+      tap(tt + 1, wb0, wb1, sb0, sb1);
+      fmac(wa0, wa1, sa0, sa1);
+      fmac(wb0, wb1, sb0, sb1);
+    }
+    if (tt < nt) {
+      T wa0, wa1;
+      Pack<T, PV> sa0[NPL], sa1[NPL];
+      tap(tt, wa0, wa1, sa0, sa1);
+      fmac(wa0, wa1, sa0, sa1);
+    }
   }
 
   double pq[VB][NQ];
@@ -467,110 +656,8 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
   for (int u = 0; u < VB; ++u)
 #pragma unroll
     for (int q = 0; q < NQ; ++q) pq[u][q] = 0.0;
+  if (inb) back_epilogue<T, VB, MODE, NQ>(A, i, j, chunk, v0, nv, acc, pq);
 
-  if (inb) {
-    if constexpr (MODE == BACK_H || MODE == BACK_INIT) {
-      // H v = acc + rho D v + mu K^T K v  (v = p or xs, interleaved samples)
-      const T* pv = A.pin + sbase;
-      T pc[VB], pn[VB];
-      double ktk[VB];
-      gload<T, VB>(pv + (size_t)pix * VB, pc);
-#pragma unroll
-      for (int u = 0; u < VB; ++u) ktk[u] = 0.0;
-      if (i >= 1) {
-        gload<T, VB>(pv + (size_t)(pix - N) * VB, pn);
-#pragma unroll
-        for (int u = 0; u < VB; ++u) ktk[u] += (double)pc[u] - (double)pn[u];
-      }
-      if (i <= N - 2) {
-        gload<T, VB>(pv + (size_t)(pix + N) * VB, pn);
-#pragma unroll
-        for (int u = 0; u < VB; ++u) ktk[u] -= (double)pn[u] - (double)pc[u];
-      }
-      if (j >= 1) {
-        gload<T, VB>(pv + (size_t)(pix - 1) * VB, pn);
-#pragma unroll
-        for (int u = 0; u < VB; ++u) ktk[u] += (double)pc[u] - (double)pn[u];
-      }
-      if (j <= N - 2) {
-        gload<T, VB>(pv + (size_t)(pix + 1) * VB, pn);
-#pragma unroll
-        for (int u = 0; u < VB; ++u) ktk[u] -= (double)pn[u] - (double)pc[u];
-      }
-      T outv[VB];
-#pragma unroll
-      for (int u = 0; u < VB; ++u) {
-        outv[u] = T(0);
-        if (u < nv) {
-          const size_t vo = (size_t)(v0 + u) * npix;
-          const double pcd = (double)pc[u];
-          const double h = (double)acc[u] + A.rho * A.dsum[vo + pix] * pcd + A.mu * ktk[u];
-          if constexpr (MODE == BACK_H) {
-            const T hp = (T)h;
-            outv[u] = hp;
-            const double hd = (double)hp;
-            const double rv = A.r[vo + pix];
-            pq[u][0] = pcd * hd;
-            pq[u][1] = rv * hd;
-            pq[u][2] = hd * hd;
-            pq[u][3] = rv * rv;
-            pq[u][4] = rv * pcd;
-          } else {
-            const double* dv = A.dvar + 2 * vo;
-            const double* ev = A.evar + 2 * vo;
-            const double rr = A.atb[vo + pix] + A.rho * A.cvec[vo + pix] + A.mu * kt_w_at(dv, ev, N, i, j) - h;
-            A.out_d[vo + pix] = rr;
-            outv[u] = (T)rr;
-          }
-        }
-      }
-      gstore<T, VB>(A.out_t + sbase + (size_t)pix * VB, outv);
-    } else if constexpr (MODE == BACK_DIAG) {
-#pragma unroll
-      for (int u = 0; u < VB; ++u) {
-        if (u >= nv) continue;
-        const int v = v0 + u;
-        const size_t vo = (size_t)v * npix;
-        const double* xv = A.x + vo;
-        const double xc = xv[pix];
-        // lam * K^T sub(Kx) at (i,j): needs the subgradient at (i,j), (i-1,j), (i,j-1)
-        double gx, gy, px, py, kts = 0.0, tvv;
-        grad_at(xv, N, i, j, gx, gy);
-        tv_sub(gx, gy, A.tv_kind, px, py);
-        tvv = (A.tv_kind == 0) ? sqrt(gx * gx + gy * gy) : fabs(gx) + fabs(gy);
-        if (i <= N - 2) kts -= px;
-        if (j <= N - 2) kts -= py;
-        if (i >= 1) {
-          double ax, ay, bx, by;
-          grad_at(xv, N, i - 1, j, ax, ay);
-          tv_sub(ax, ay, A.tv_kind, bx, by);
-          kts += bx;
-        }
-        if (j >= 1) {
-          double ax, ay, bx, by;
-          grad_at(xv, N, i, j - 1, ax, ay);
-          tv_sub(ax, ay, A.tv_kind, bx, by);
-          kts += by;
-        }
-        const double cc = A.cvec[vo + pix];
-        const double g = (double)acc[u] + A.rho * (A.dsum[vo + pix] * xc - cc) + A.lam * kts;
-        double quad = 0.0;
-        for (int q = A.inc_off[v]; q < A.inc_off[v + 1]; ++q) {
-          const size_t eo = (size_t)A.inc_edge[q] * npix + pix;
-          const double vij = A.zv[eo] - (double)A.inc_sign[q] * A.yv[eo];
-          const double dd = xc - vij;
-          quad += A.qv[(size_t)A.inc_qslot[q] * npix + pix] * dd * dd;
-        }
-        pq[u][0] = g * g;
-        pq[u][1] = tvv;
-        pq[u][2] = 0.5 * A.rho * quad;
-        if (A.phantom) {
-          const double dp = xc - A.phantom[pix];
-          pq[u][3] = dp * dp;
-        }
-      }
-    }
-  }
   if constexpr (MODE == BACK_H || MODE == BACK_DIAG) {
     constexpr int NV = ((VB * NQ + 15) / 16) * 16;
     __shared__ double lds[4 * NV];
@@ -593,30 +680,37 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
 }
 
 // ===========================================================================
-// 32x32-tile elementwise kernels (block 256 = 32 (j) x 8 (i), rows ty + 8r).
-// Sample outputs are written row-major AND transposed (through an LDS tile of
-// VB-vectors), because the forward projector reads the transposed copy for
-// case-A angles.  blockIdx.z = node chunk.
+// Elementwise kernels, node-parallel: a block covers a 32 (j) x 32/VB (i) tile
+// of VB nodes; its 256 threads are VB (node, fastest) x 32 (j) x 8/VB (row phase)
+// and each handles one (pixel, node) in each of 4 rows.  Interleaved sample
+// stores are contiguous across lanes and a launch has VB x more waves than a
+// pixel-per-thread mapping.  Sample outputs are written row-major AND transposed
+// (through a 4 KB LDS tile; every transposed row run is 32 samples = one 128-B
+// line for float), because the forward projector reads the transposed copy for
+// case-A angles.  blockIdx.z = chunk.
 // ===========================================================================
-template <typename T, int VB>
-struct TileT {
-  Pack<T, VB> t[kTile][kTile + 1];
+template <int VB>
+struct EwMap {
+  static constexpr int TI = kTile / VB;  // tile rows
+  static constexpr int RPI = 8 / VB;     // rows per iteration
+  int u, jj, isub;
+  __device__ EwMap() : u(threadIdx.x % VB), jj((threadIdx.x / VB) % kTile), isub(threadIdx.x / (kTile * VB)) {}
 };
 
 template <typename T, int VB>
-__device__ __forceinline__ void tile_put(TileT<T, VB>& tl, int r, int c, const T (&v)[VB]) {
-#pragma unroll
-  for (int u = 0; u < VB; ++u) tl.t[r][c].v[u] = v[u];
-}
+struct TileT {
+  T t[EwMap<VB>::TI][kTile + 1][VB];
+};
 
-// outT (interleaved, chunk base applied by caller): outT[j][i] = tile[i - i0][j - j0]
+// outT (interleaved, chunk base applied by caller): outT[j][i][u] = tile[i - i0][j - j0][u]
 template <typename T, int VB>
 __device__ __forceinline__ void tile_store_T(TileT<T, VB>& tl, T* __restrict__ outT, int N, int i0, int j0) {
+  constexpr int TI = EwMap<VB>::TI;
   __syncthreads();
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (int r = ty; r < kTile; r += 8) {
-    const int jj = j0 + r, ii = i0 + tx;
-    if (jj < N && ii < N) *reinterpret_cast<Pack<T, VB>*>(outT + ((size_t)jj * N + ii) * VB) = tl.t[tx][r];
+  const int u = threadIdx.x % VB, r = (threadIdx.x / VB) % TI, c0 = threadIdx.x / (VB * TI);
+  for (int c = c0; c < kTile; c += kBlock / (VB * TI)) {
+    const int jj = j0 + c, ii = i0 + r;
+    if (jj < N && ii < N) outT[((size_t)jj * N + ii) * VB + u] = tl.t[r][c][u];
   }
 }
 
@@ -630,33 +724,30 @@ __global__ __launch_bounds__(kBlock) void k_gather(const double* __restrict__ x,
                                                    const int* __restrict__ inc_sign, double* __restrict__ c,
                                                    T* __restrict__ xs, T* __restrict__ xsT, int N, int V) {
   __shared__ TileT<T, VB> tl;
-  const int chunk = blockIdx.z, v0 = chunk * VB, nv = min(VB, V - v0);
+  const EwMap<VB> mp;
+  const int chunk = blockIdx.z, v = chunk * VB + mp.u;
+  const bool live = v < V;
   const int npix = N * N;
   const size_t sbase = (size_t)chunk * npix * VB;
-  const int i0 = blockIdx.y * kTile, j0 = blockIdx.x * kTile;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (int r = ty; r < kTile; r += 8) {
-    const int i = i0 + r, j = j0 + tx;
+  const int i0 = blockIdx.y * EwMap<VB>::TI, j0 = blockIdx.x * kTile;
+  const int e0 = live ? inc_off[v] : 0, e1 = live ? inc_off[v + 1] : 0;
+  for (int r = mp.isub; r < EwMap<VB>::TI; r += EwMap<VB>::RPI) {
+    const int i = i0 + r, j = j0 + mp.jj;
     if (i < N && j < N) {
       const int pix = i * N + j;
-      T s[VB];
-#pragma unroll
-      for (int u = 0; u < VB; ++u) {
-        s[u] = T(0);
-        if (u < nv) {
-          const int v = v0 + u;
-          double acc = 0.0;
-          for (int qq = inc_off[v]; qq < inc_off[v + 1]; ++qq) {
-            const size_t eo = (size_t)inc_edge[qq] * npix + pix;
-            const double vij = z[eo] - (double)inc_sign[qq] * y[eo];
-            acc += q[(size_t)inc_qslot[qq] * npix + pix] * vij;
-          }
-          c[(size_t)v * npix + pix] = acc;
-          s[u] = (T)x[(size_t)v * npix + pix];
+      T sv = T(0);
+      if (live) {
+        double acc = 0.0;
+        for (int qq = e0; qq < e1; ++qq) {
+          const size_t eo = (size_t)inc_edge[qq] * npix + pix;
+          const double vij = z[eo] - (double)inc_sign[qq] * y[eo];
+          acc += q[(size_t)inc_qslot[qq] * npix + pix] * vij;
         }
+        c[(size_t)v * npix + pix] = acc;
+        sv = (T)x[(size_t)v * npix + pix];
       }
-      gstore<T, VB>(xs + sbase + (size_t)pix * VB, s);
-      tile_put<T, VB>(tl, r, tx, s);
+      xs[sbase + (size_t)pix * VB + mp.u] = sv;
+      tl.t[r][mp.jj][mp.u] = sv;
     }
   }
   tile_store_T<T, VB>(tl, xsT + sbase, N, i0, j0);
@@ -665,12 +756,12 @@ __global__ __launch_bounds__(kBlock) void k_gather(const double* __restrict__ x,
 template <typename T, int VB>
 __global__ __launch_bounds__(kBlock) void k_transpose(const T* __restrict__ in, T* __restrict__ outT, int N) {
   __shared__ TileT<T, VB> tl;
+  const EwMap<VB> mp;
   const size_t sbase = (size_t)blockIdx.z * N * N * VB;
-  const int i0 = blockIdx.y * kTile, j0 = blockIdx.x * kTile;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (int r = ty; r < kTile; r += 8) {
-    const int i = i0 + r, j = j0 + tx;
-    if (i < N && j < N) tl.t[r][tx] = *reinterpret_cast<const Pack<T, VB>*>(in + sbase + ((size_t)i * N + j) * VB);
+  const int i0 = blockIdx.y * EwMap<VB>::TI, j0 = blockIdx.x * kTile;
+  for (int r = mp.isub; r < EwMap<VB>::TI; r += EwMap<VB>::RPI) {
+    const int i = i0 + r, j = j0 + mp.jj;
+    if (i < N && j < N) tl.t[r][mp.jj][mp.u] = in[sbase + ((size_t)i * N + j) * VB + mp.u];
   }
   tile_store_T<T, VB>(tl, outT + sbase, N, i0, j0);
 }
@@ -684,48 +775,37 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(double* __restrict__ x, do
                                                       const T* __restrict__ Hp, const double* __restrict__ redH,
                                                       int N, int V) {
   __shared__ TileT<T, VB> tl;
-  const int chunk = blockIdx.z, v0 = chunk * VB, nv = min(VB, V - v0);
+  const EwMap<VB> mp;
+  const int chunk = blockIdx.z, v = chunk * VB + mp.u;
+  const bool live = v < V;
   const int npix = N * N;
   const size_t sbase = (size_t)chunk * npix * VB;
-  double alpha[VB], beta[VB];
-#pragma unroll
-  for (int u = 0; u < VB; ++u) {
-    alpha[u] = 0.0;
-    beta[u] = 0.0;
-    if (u < nv) {
-      const int v = v0 + u;
-      const double* S = redH + 5 * v;
-      const double pHp = S[0], rHp = S[1], HH = S[2], rr = S[3], rp = S[4];
-      const double al = (pHp != 0.0) ? rp / pHp : 0.0;
-      double rrn = rr - 2.0 * al * rHp + al * al * HH;
-      rrn = fmax(rrn, 0.0);
-      alpha[u] = al;
-      beta[u] = (rr != 0.0) ? rrn / rr : 0.0;
-    }
+  double alpha = 0.0, beta = 0.0;
+  if (live) {
+    const double* S = redH + 5 * v;
+    const double pHp = S[0], rHp = S[1], HH = S[2], rr = S[3], rp = S[4];
+    alpha = (pHp != 0.0) ? rp / pHp : 0.0;
+    double rrn = rr - 2.0 * alpha * rHp + alpha * alpha * HH;
+    rrn = fmax(rrn, 0.0);
+    beta = (rr != 0.0) ? rrn / rr : 0.0;
   }
-  const int i0 = blockIdx.y * kTile, j0 = blockIdx.x * kTile;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (int rw = ty; rw < kTile; rw += 8) {
-    const int i = i0 + rw, j = j0 + tx;
+  const int i0 = blockIdx.y * EwMap<VB>::TI, j0 = blockIdx.x * kTile;
+  for (int rw = mp.isub; rw < EwMap<VB>::TI; rw += EwMap<VB>::RPI) {
+    const int i = i0 + rw, j = j0 + mp.jj;
     if (i < N && j < N) {
       const int pix = i * N + j;
-      T pv[VB], hv[VB], np[VB];
-      gload<T, VB>(p + sbase + (size_t)pix * VB, pv);
-      gload<T, VB>(Hp + sbase + (size_t)pix * VB, hv);
-#pragma unroll
-      for (int u = 0; u < VB; ++u) {
-        np[u] = T(0);
-        if (u < nv) {
-          const size_t o = (size_t)(v0 + u) * npix + pix;
-          const double pd = (double)pv[u];
-          x[o] += alpha[u] * pd;
-          const double rn = r[o] - alpha[u] * (double)hv[u];
-          r[o] = rn;
-          np[u] = (T)(rn + beta[u] * pd);
-        }
+      const size_t so = sbase + (size_t)pix * VB + mp.u;
+      T np = T(0);
+      if (live) {
+        const size_t o = (size_t)v * npix + pix;
+        const double pd = (double)p[so];
+        x[o] += alpha * pd;
+        const double rn = r[o] - alpha * (double)Hp[so];
+        r[o] = rn;
+        np = (T)(rn + beta * pd);
       }
-      gstore<T, VB>(p + sbase + (size_t)pix * VB, np);
-      tile_put<T, VB>(tl, rw, tx, np);
+      p[so] = np;
+      tl.t[rw][mp.jj][mp.u] = np;
     }
   }
   tile_store_T<T, VB>(tl, pT + sbase, N, i0, j0);
@@ -756,24 +836,22 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
                                                       T* __restrict__ p, T* __restrict__ pT, double tau,
                                                       double mu, int kind, int N, int V) {
   __shared__ TileT<T, VB> tl;
-  const int chunk = blockIdx.z, v0 = chunk * VB, nv = min(VB, V - v0);
+  const EwMap<VB> mp;
+  const int chunk = blockIdx.z, v = chunk * VB + mp.u;
+  const bool live = v < V;
   const int npix = N * N;
   const size_t sbase = (size_t)chunk * npix * VB;
-  const int i0 = blockIdx.y * kTile, j0 = blockIdx.x * kTile;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (int rw = ty; rw < kTile; rw += 8) {
-    const int i = i0 + rw, j = j0 + tx;
+  const int i0 = blockIdx.y * EwMap<VB>::TI, j0 = blockIdx.x * kTile;
+  const size_t vo = (size_t)(live ? v : 0) * npix;
+  const double* xv = x + vo;
+  const double* dv = din + 2 * vo;
+  const double* ev = ein + 2 * vo;
+  for (int rw = mp.isub; rw < EwMap<VB>::TI; rw += EwMap<VB>::RPI) {
+    const int i = i0 + rw, j = j0 + mp.jj;
     if (i >= N || j >= N) continue;
     const int o = i * N + j;
-    T sv[VB];
-#pragma unroll
-    for (int u = 0; u < VB; ++u) {
-      sv[u] = T(0);
-      if (u >= nv) continue;
-      const size_t vo = (size_t)(v0 + u) * npix;
-      const double* xv = x + vo;
-      const double* dv = din + 2 * vo;
-      const double* ev = ein + 2 * vo;
+    T sv = T(0);
+    if (live) {
       double gx, gy, ux, uy, ndx, ndy;
       grad_at(xv, N, i, j, gx, gy);
       ux = gx + ev[o];
@@ -807,13 +885,13 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
         }
         const double rn = r[vo + o] + mu * kt;
         r[vo + o] = rn;
-        sv[u] = (T)rn;
+        sv = (T)rn;
       } else {
-        sv[u] = (T)xv[o];
+        sv = (T)xv[o];
       }
     }
-    gstore<T, VB>(p + sbase + (size_t)o * VB, sv);
-    tile_put<T, VB>(tl, rw, tx, sv);
+    p[sbase + (size_t)o * VB + mp.u] = sv;
+    tl.t[rw][mp.jj][mp.u] = sv;
   }
   tile_store_T<T, VB>(tl, pT + sbase, N, i0, j0);
 }
