@@ -175,7 +175,7 @@ def main():
             "graph": "ring", "parallelism": f"graph-node shards x{world}",
         },
         "roofline": {
-            "kernel": "k_fwd<float,8,0> (Joseph forward projector)",
+            "kernel": "k_fwdg<float,8> + k_fwd_combine<float,8,0> (Joseph forward projector, angle-grouped)",
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,

@@ -6,6 +6,7 @@
 // otherwise: ~170 kernels per x-update).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -66,6 +67,8 @@ struct admm_ctx {
   int npix = 0, mrays = 0;
   FwdAngle* fang = nullptr;
   BackAngle* bang = nullptr;
+  FgGroup* groups = nullptr;  // angle groups of the grouped forward projector
+  int n_groups = 0;           // 0: geometry does not fit the grouped kernel -> k_fwd
   hipStream_t cap = nullptr;  // private capture stream
 
   // operator-API scratch
@@ -75,7 +78,7 @@ struct admm_ctx {
   bool bound = false;
   admm_batch b{};
   int vb = 1;  // node interleave width of the sample buffers
-  Buf xs, xsT, p, pT, Hp, sino, bI, r, c, d2, e2;
+  Buf xs, xsT, p, pT, Hp, sino, bI, fpart, r, c, d2, e2;
   Buf partH, partS, partD, partE;
   Buf redH;
   int P_back = 0, P_tile = 0, P_fwd = 0, P_edge = 0;
@@ -109,6 +112,23 @@ int launch_fwd(admm_ctx* C, const T* img, const T* imgT, T* sino, const T* b, do
   dim3 grid((C->g.n_det + kFwdRays - 1) / kFwdRays, C->g.n_angles, (V + VB - 1) / VB);
   hipLaunchKernelGGL((k_fwd<T, VB, MODE>), grid, dim3(kFwdBlock), 0, s, img, imgT, sino, b, part, C->fang, C->g.N,
                      C->g.n_det, C->g.n_angles, V);
+  CHECK_LAUNCH();
+  return ADMM_OK;
+}
+
+// hot-path forward projection of the bound batch: grouped kernel + fixed-order combine
+template <typename T, int VB, int MODE>
+int launch_fwd_batch(admm_ctx* C, const T* img, const T* imgT, T* sino, const T* b, double* part, int V,
+                     hipStream_t s) {
+  if (C->n_groups == 0) return launch_fwd<T, VB, MODE>(C, img, imgT, sino, b, part, V, s);
+  const int nch = (V + VB - 1) / VB;
+  dim3 grid((C->g.n_det + 63) / 64, C->n_groups, nch * kFgSeg);
+  hipLaunchKernelGGL((k_fwdg<T, VB>), grid, dim3(kBlock), 0, s, img, imgT, (T*)C->fpart.p, C->fang, C->groups,
+                     C->g.N, C->g.n_det, C->g.n_angles, V);
+  CHECK_LAUNCH();
+  dim3 cg((C->mrays + kBlock - 1) / kBlock, nch);
+  hipLaunchKernelGGL((k_fwd_combine<T, VB, MODE>), cg, dim3(kBlock), 0, s, (const T*)C->fpart.p, sino, b, part,
+                     C->fang, C->g.n_det, C->g.n_angles, V);
   CHECK_LAUNCH();
   return ADMM_OK;
 }
@@ -168,7 +188,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
                      B.inc_qslot, B.inc_sign, c, xs, xsT, N, V);
   CHECK_LAUNCH();
   // 2-4. r = A^T b + rho c + mu K^T(d - e) - H x,  p = r,  rr
-  RET((launch_fwd<T, VB, 0>(C, xs, xsT, sino, nullptr, nullptr, V, s)));
+  RET((launch_fwd_batch<T, VB, 0>(C, xs, xsT, sino, nullptr, nullptr, V, s)));
   {
     BackArgs<T> a{};
     a.sino = sino;
@@ -196,7 +216,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
   const int K = B.cg_iters, Tt = B.tv_iters;
   for (int t = 0; t < Tt; ++t) {
     for (int kk = 0; kk < K; ++kk) {
-      RET((launch_fwd<T, VB, 0>(C, p, pT, sino, nullptr, nullptr, V, s)));
+      RET((launch_fwd_batch<T, VB, 0>(C, p, pT, sino, nullptr, nullptr, V, s)));
       BackArgs<T> a{};
       a.sino = sino;
       a.out_t = Hp;
@@ -230,7 +250,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
     HIPCHK(hipMemcpyAsync(B.e, ecur, 2 * V * npix * sizeof(double), hipMemcpyDeviceToDevice, s));
   }
   // diagnostics epilogue: s = A x - b, ||s||^2, g, TV, quad, image error
-  RET((launch_fwd<T, VB, 1>(C, xs, xsT, sino, (const T*)B.b, (double*)C->partS.p, V, s)));
+  RET((launch_fwd_batch<T, VB, 1>(C, xs, xsT, sino, (const T*)B.b, (double*)C->partS.p, V, s)));
   {
     BackArgs<T> a{};
     a.sino = sino;
@@ -317,6 +337,7 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
   *out = nullptr;
   const admm_geom g = *geom;
   if (g.N < 2 || g.n_angles < 1 || g.n_det < 1) return fail(ADMM_E_INVALID, "bad geometry sizes");
+  if (g.N > 4096) return fail(ADMM_E_INVALID, "N > 4096 is not supported");
   if (dtype != ADMM_DTYPE_F32 && dtype != ADMM_DTYPE_F64) return fail(ADMM_E_INVALID, "bad dtype");
   if (max_images < 1) return fail(ADMM_E_INVALID, "max_images < 1");
   const double h = 2.0 / g.N;
@@ -359,6 +380,43 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
     ba[t].slope = (hd / h) / std::fabs(al);
     ba[t].L = h / std::fabs(al);
   }
+  // angle groups for the grouped forward projector: consecutive angles of one case,
+  // G <= 4, such that the union row window of a 64-ray chunk fits kFgWin (float64,
+  // same formulas as the device; 2 pixels of margin).
+  std::vector<FgGroup> groups;
+  bool fits = true;
+  {
+    const int nkc = (g.n_det + 63) / 64;
+    auto width_ok = [&](int t0, int G) {
+      for (int q = 0; q < G; ++q)
+        if (fa[t0 + q].caseA != fa[t0].caseA) return false;
+      for (int kc = 0; kc < nkc; ++kc) {
+        const int ks[2] = {kc * 64, std::min(kc * 64 + 63, g.n_det - 1)};
+        for (int m = 0; m < g.N; ++m) {
+          double lo = 1e300, hi = -1e300;
+          for (int q = 0; q < G; ++q)
+            for (int kk : ks) {
+              const double l = std::fma((double)m, fa[t0 + q].dl, std::fma((double)kk, fa[t0 + q].A1, fa[t0 + q].A0));
+              lo = std::min(lo, l);
+              hi = std::max(hi, l);
+            }
+          if (std::floor(hi) - std::floor(lo) + 2 > kFgWin - 2) return false;
+        }
+      }
+      return true;
+    };
+    for (int t0 = 0; t0 < g.n_angles;) {
+      int G = std::min(4, g.n_angles - t0);
+      while (G > 1 && !width_ok(t0, G)) --G;
+      if (G == 1 && !width_ok(t0, 1)) {
+        fits = false;
+        break;
+      }
+      groups.push_back(FgGroup{t0, G});
+      t0 += G;
+    }
+    if (getenv("ADMM_NO_FWDG") && getenv("ADMM_NO_FWDG")[0] == '1') fits = false;
+  }
   hipError_t e1 = hipMalloc(&C->fang, fa.size() * sizeof(FwdAngle));
   hipError_t e2 = hipMalloc(&C->bang, ba.size() * sizeof(BackAngle));
   if (e1 != hipSuccess || e2 != hipSuccess) {
@@ -367,6 +425,11 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
   }
   HIPCHK(hipMemcpy(C->fang, fa.data(), fa.size() * sizeof(FwdAngle), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(C->bang, ba.data(), ba.size() * sizeof(BackAngle), hipMemcpyHostToDevice));
+  if (fits && !groups.empty()) {
+    HIPCHK(hipMalloc(&C->groups, groups.size() * sizeof(FgGroup)));
+    HIPCHK(hipMemcpy(C->groups, groups.data(), groups.size() * sizeof(FgGroup), hipMemcpyHostToDevice));
+    C->n_groups = (int)groups.size();
+  }
   HIPCHK(hipStreamCreateWithFlags(&C->cap, hipStreamNonBlocking));
   *out = C;
   return ADMM_OK;
@@ -377,12 +440,13 @@ int admm_ctx_destroy(admm_ctx* C) {
   (void)hipSetDevice(C->device);
   (void)hipDeviceSynchronize();
   free_graphs(C);
-  Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->bI, &C->r, &C->c,
+  Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->bI, &C->fpart, &C->r, &C->c,
                  &C->d2, &C->e2, &C->partH, &C->partS, &C->partD, &C->partE, &C->redH};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (C->fang) (void)hipFree(C->fang);
   if (C->bang) (void)hipFree(C->bang);
+  if (C->groups) (void)hipFree(C->groups);
   if (C->cap) (void)hipStreamDestroy(C->cap);
   delete C;
   return ADMM_OK;
@@ -489,6 +553,7 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   RET(ensure(C->Hp, Vp * npix * ds));
   RET(ensure(C->sino, Vp * m * ds));
   RET(ensure(C->bI, Vp * m * ds));
+  if (C->n_groups > 0) RET(ensure(C->fpart, (size_t)kFgSeg * Vp * m * ds));
   RET(ensure(C->r, V * npix * 8));
   RET(ensure(C->c, V * npix * 8));
   RET(ensure(C->d2, 2 * V * npix * 8));
@@ -498,7 +563,8 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   C->P_tile = ((N + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
   if ((size_t)Vp * npix * ds >= (1ull << 31) || (size_t)Vp * m * ds >= (1ull << 31))
     return fail(ADMM_E_INVALID, "batch too large for 32-bit buffer offsets");
-  C->P_fwd = ((C->g.n_det + kFwdRays - 1) / kFwdRays) * C->g.n_angles;
+  C->P_fwd = C->n_groups > 0 ? (int)((m + kBlock - 1) / kBlock)
+                             : ((C->g.n_det + kFwdRays - 1) / kFwdRays) * C->g.n_angles;
   C->P_edge = (int)((npix + kBlock * 4 - 1) / (kBlock * 4));
   RET(ensure(C->partH, (size_t)5 * V * C->P_back * 8));
   RET(ensure(C->partS, (size_t)V * C->P_fwd * 8));
@@ -573,10 +639,10 @@ int time_fwd(admm_ctx* C, int reps, hipStream_t s, float* ms) {
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
-    RET((launch_fwd<T, VB, 0>(C, (T*)C->xs.p, (T*)C->xsT.p, (T*)C->sino.p, nullptr, nullptr, C->b.V, s)));
+    RET((launch_fwd_batch<T, VB, 0>(C, (T*)C->xs.p, (T*)C->xsT.p, (T*)C->sino.p, nullptr, nullptr, C->b.V, s)));
     HIPCHK(hipEventRecord(e0, s));
     for (int i = 0; i < reps; ++i)
-      RET((launch_fwd<T, VB, 0>(C, (T*)C->xs.p, (T*)C->xsT.p, (T*)C->sino.p, nullptr, nullptr, C->b.V, s)));
+      RET((launch_fwd_batch<T, VB, 0>(C, (T*)C->xs.p, (T*)C->xsT.p, (T*)C->sino.p, nullptr, nullptr, C->b.V, s)));
     HIPCHK(hipEventRecord(e1, s));
     HIPCHK(hipEventSynchronize(e1));
     HIPCHK(hipEventElapsedTime(ms, e0, e1));

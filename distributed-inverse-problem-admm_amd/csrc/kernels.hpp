@@ -85,6 +85,13 @@ struct alignas((VB * sizeof(T)) >= 16 ? 16 : (VB * sizeof(T))) Pack {
 };
 
 template <typename T, int VB>
+struct Planes {
+  static constexpr int BYTES = VB * (int)sizeof(T);
+  static constexpr int NPL = BYTES > 16 ? BYTES / 16 : 1;  // 16-byte planes
+  static constexpr int PV = VB / NPL;                      // values per plane
+};
+
+template <typename T, int VB>
 __device__ __forceinline__ void gload(const T* __restrict__ p, T (&o)[VB]) {
   const Pack<T, VB> k = *reinterpret_cast<const Pack<T, VB>*>(p);
 #pragma unroll
@@ -323,6 +330,176 @@ __global__ __launch_bounds__(kFwdBlock) void k_fwd(const T* __restrict__ img, co
 }
 
 // ===========================================================================
+// Forward projector, angle-grouped (the hot-path version).
+// Block = G <= 4 consecutive angles of one case (one wave each) x 64 consecutive
+// detector bins, over one of kFgSeg row segments.  Rows are processed in chunks of
+// kFgRows: for each row the block stages into LDS the window of image pixels
+// (columns wlo .. wlo+kFgWin-1) that any of its G x 64 rays can touch, zero-filled
+// outside the image, then every ray takes its two taps per row from LDS.  One
+// staged pixel serves ~G x 1.4 x 2 taps, so texture-path traffic drops ~G-fold
+// and taps run at LDS rate.  The host sizes groups so the window fits
+// (FgGroup tables; wider N -> smaller G).  Segment partial sums go to
+// part[seg][chunk][ray][VB] and k_fwd_combine adds them in fixed order.
+// ===========================================================================
+constexpr int kFgRows = 8;
+constexpr int kFgWin = 160;
+constexpr int kFgSeg = 4;
+
+struct FgGroup {
+  int t0, G;
+};
+
+template <typename T, int VB>
+__global__ __launch_bounds__(kBlock) void k_fwdg(const T* __restrict__ img, const T* __restrict__ imgT,
+                                                 T* __restrict__ part, const FwdAngle* __restrict__ ang,
+                                                 const FgGroup* __restrict__ groups, int N, int n_det, int n_ang,
+                                                 int V) {
+  constexpr int NPL = Planes<T, VB>::NPL, PV = Planes<T, VB>::PV;
+  constexpr int PER = (kFgRows * kFgWin * NPL + kBlock - 1) / kBlock;  // staged packs per thread
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int kc = blockIdx.x;
+  const FgGroup gr = groups[blockIdx.y];
+  const int seg = blockIdx.z % kFgSeg, chunk = blockIdx.z / kFgSeg;
+  const int npix = N * N;
+  const int k = kc * 64 + lane;
+  const int kcl = min(k, n_det - 1);
+  const int t = gr.t0 + min(g, gr.G - 1);
+  const FwdAngle a = ang[t];
+  const T* src = (ang[gr.t0].caseA ? imgT : img) + (size_t)chunk * npix * VB;
+  const double l0 = fma((double)kcl, a.A1, a.A0);
+  const int klo = kc * 64, khi = min(kc * 64 + 63, n_det - 1);
+  const int m_lo = seg * N / kFgSeg, m_hi = (seg + 1) * N / kFgSeg;
+  const int nrows = m_hi - m_lo;
+
+  __shared__ Pack<T, PV> win[NPL][kFgRows][kFgWin];
+  __shared__ int wlo_s[(4096 + kFgSeg - 1) / kFgSeg];  // every row window of the segment (N <= 4096)
+  for (int r = threadIdx.x; r < nrows; r += kBlock) {
+    const double dm = (double)(m_lo + r);
+    double lmin = 1e300;
+    for (int gg = 0; gg < gr.G; ++gg) {
+      const FwdAngle b = ang[gr.t0 + gg];
+      lmin = fmin(lmin, fma(dm, b.dl, fma((double)klo, b.A1, b.A0)));
+      lmin = fmin(lmin, fma(dm, b.dl, fma((double)khi, b.A1, b.A0)));
+    }
+    wlo_s[r] = (int)floor(lmin) - 1;
+  }
+  __syncthreads();
+
+  // staging in two halves: issue global loads for chunk c+1 into registers
+  // (prefetch), compute chunk c from LDS, then write the registers into LDS.
+  Pack<T, PV> stage[PER];
+  auto fetch = [&](int m0) {
+    const int rows = min(kFgRows, m_hi - m0);
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int q = threadIdx.x + e * kBlock;
+      const int pl = q % NPL, rw = q / NPL;
+      const int r = rw / kFgWin, w = rw - r * kFgWin;
+      const int col = (r < rows) ? wlo_s[m0 - m_lo + r] + w : -1;
+      if (q < kFgRows * kFgWin * NPL && col >= 0 && col < N) {
+        stage[e] = *reinterpret_cast<const Pack<T, PV>*>(src + ((size_t)(m0 + r) * N + col) * VB + pl * PV);
+      } else {
+#pragma unroll
+        for (int z = 0; z < PV; ++z) stage[e].v[z] = T(0);
+      }
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int q = threadIdx.x + e * kBlock;
+      if (q < kFgRows * kFgWin * NPL) {
+        const int pl = q % NPL, rw = q / NPL;
+        const int r = rw / kFgWin, w = rw - r * kFgWin;
+        win[pl][r][w] = stage[e];
+      }
+    }
+  };
+
+  T acc[VB];
+#pragma unroll
+  for (int u = 0; u < VB; ++u) acc[u] = T(0);
+  fetch(m_lo);
+  for (int m0 = m_lo; m0 < m_hi; m0 += kFgRows) {
+    const int rows = min(kFgRows, m_hi - m0);
+    __syncthreads();  // previous chunk's readers are done
+    commit();
+    __syncthreads();
+    if (m0 + kFgRows < m_hi) fetch(m0 + kFgRows);
+    for (int r = 0; r < rows; ++r) {
+      const double l = fma((double)(m0 + r), a.dl, l0);
+      const double fl = floor(l);
+      const int idx = (int)fl - wlo_s[m0 - m_lo + r];
+      const T w1 = (T)(l - fl);
+      const T w0 = T(1) - w1;
+#pragma unroll
+      for (int q = 0; q < NPL; ++q) {
+        const Pack<T, PV> s0 = win[q][r][idx];
+        const Pack<T, PV> s1 = win[q][r][idx + 1];
+#pragma unroll
+        for (int e = 0; e < PV; ++e) {
+          acc[q * PV + e] = fma(w0, s0.v[e], acc[q * PV + e]);
+          acc[q * PV + e] = fma(w1, s1.v[e], acc[q * PV + e]);
+        }
+      }
+    }
+  }
+  if (g < gr.G && k < n_det) {
+    const size_t m_rays = (size_t)n_ang * n_det;
+    gstore<T, VB>(part + (((size_t)seg * ((V + VB - 1) / VB) + chunk) * m_rays + (size_t)t * n_det + k) * VB, acc);
+  }
+}
+
+// Sum the kFgSeg segment partials in fixed order, scale by L(t):
+// MODE 0: sino = A x.  MODE 1: s = A x - b (b node-major) + per-block partials of ||s||^2.
+template <typename T, int VB, int MODE>
+__global__ __launch_bounds__(kBlock) void k_fwd_combine(const T* __restrict__ part, T* __restrict__ sino,
+                                                        const T* __restrict__ bsino, double* __restrict__ pout,
+                                                        const FwdAngle* __restrict__ ang, int n_det, int n_ang,
+                                                        int V) {
+  const int chunk = blockIdx.y, v0 = chunk * VB, nv = min(VB, V - v0);
+  const int nch = (V + VB - 1) / VB;
+  const size_t m_rays = (size_t)n_ang * n_det;
+  const size_t ray = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  double sq[VB];
+#pragma unroll
+  for (int u = 0; u < VB; ++u) sq[u] = 0.0;
+  if (ray < m_rays) {
+    const T L = (T)ang[ray / n_det].L;
+    T acc[VB], pv[VB];
+    gload<T, VB>(part + ((size_t)chunk * m_rays + ray) * VB, acc);
+#pragma unroll
+    for (int sg = 1; sg < kFgSeg; ++sg) {
+      gload<T, VB>(part + (((size_t)sg * nch + chunk) * m_rays + ray) * VB, pv);
+#pragma unroll
+      for (int u = 0; u < VB; ++u) acc[u] += pv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < VB; ++u) {
+      acc[u] *= L;
+      if (MODE == 1) {
+        if (u < nv) {
+          acc[u] -= bsino[(size_t)(v0 + u) * m_rays + ray];
+          sq[u] = (double)acc[u] * (double)acc[u];
+        } else {
+          acc[u] = T(0);
+        }
+      }
+    }
+    gstore<T, VB>(sino + ((size_t)chunk * m_rays + ray) * VB, acc);
+  }
+  if (MODE == 1) {
+    __shared__ double lds[4 * VB];
+    block_reduce<VB>(sq, lds);
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int u = 0; u < VB; ++u)
+        if (u < nv) pout[(size_t)(v0 + u) * gridDim.x + blockIdx.x] = sq[u];
+    }
+  }
+}
+
+// ===========================================================================
 // Back projector (pixel-driven gather; exact transpose of the Joseph weights):
 //   acc[v][i,j] = sum_t sum_{k in {k0,k0+1}} w_t(k) * sino[v][t][k]
 // Replaces `Ai.T @ r` (block_6_admm_loop_ver2.py:145).  No atomics: each pixel
@@ -537,13 +714,6 @@ constexpr int kBTJ = 64;
 constexpr int kBTI = 4;
 constexpr int kBAngC = 16;
 constexpr int kBWin = 72;
-
-template <typename T, int VB>
-struct Planes {
-  static constexpr int BYTES = VB * (int)sizeof(T);
-  static constexpr int NPL = BYTES > 16 ? BYTES / 16 : 1;  // 16-byte planes
-  static constexpr int PV = VB / NPL;                      // values per plane
-};
 
 template <typename T, int VB, int MODE>
 __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
@@ -829,6 +999,15 @@ __device__ __forceinline__ void shrink2(double ux, double uy, double tau, int ki
   }
 }
 
+// XCD-aware tile order (performance only): workgroups are dealt round-robin over the 8 XCDs,
+// so consecutive ids land on different L2s.  Remap so that the ids sharing an XCD (orig % 8)
+// get one contiguous run of tiles; a stencil's halo rows/columns are then fetched by the
+// same L2.  Bijective for any nwg (guide: cdna_hip_programming.md, XCD swizzle).
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
 template <typename T, int VB, bool LAST>
 __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__ x, const double* __restrict__ din,
                                                       const double* __restrict__ ein, double* __restrict__ dout,
@@ -841,7 +1020,8 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
   const bool live = v < V;
   const int npix = N * N;
   const size_t sbase = (size_t)chunk * npix * VB;
-  const int i0 = blockIdx.y * EwMap<VB>::TI, j0 = blockIdx.x * kTile;
+  const int wg = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int i0 = (wg / gridDim.x) * EwMap<VB>::TI, j0 = (wg % gridDim.x) * kTile;
   const size_t vo = (size_t)(live ? v : 0) * npix;
   const double* xv = x + vo;
   const double* dv = din + 2 * vo;
