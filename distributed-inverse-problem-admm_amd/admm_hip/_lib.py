@@ -17,6 +17,15 @@ ADMM_DTYPE_F32 = 0
 ADMM_DTYPE_F64 = 1
 ADMM_TV_ISO = 0
 ADMM_TV_ANISO = 1
+ADMM_FUSE_MIDPOINT = 0
+ADMM_FUSE_WEIGHTED = 1
+ABI_VERSION = 2
+ADMM_MASK_KNN = 0
+ADMM_MASK_MST = 1
+ADMM_MASK_CHAIN = 2
+ADMM_Q_ARITHMETIC = 0
+ADMM_Q_HARMONIC = 1
+MASK_MAX_NODES = 64
 NODE_STATS = 5  # mse_sino, |g|^2, TV, quad, img
 EDGE_STATS = 3  # |x_a-z|^2, |x_b-z|^2, |dz|^2
 
@@ -71,6 +80,10 @@ class Batch(C.Structure):
         ("inc_sign", C.c_void_p),
         ("node_stats", C.c_void_p),
         ("edge_stats", C.c_void_p),
+        ("fusion", C.c_int32),
+        ("reserved2", C.c_int32),
+        ("y_b", C.c_void_p),
+        ("w", C.c_void_p),
     ]
 
 
@@ -90,6 +103,10 @@ SYMBOLS = {
     "admm_node_update": [C.c_void_p, C.c_void_p],
     "admm_consensus": [C.c_void_p, C.c_void_p],
     "admm_time_forward": [C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_double)],
+    "admm_pixel_masks": [C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                         C.c_void_p, C.c_void_p],
+    "admm_chain_orders": [C.POINTER(C.c_uint64), C.c_int, C.c_uint32, C.c_int, C.c_int64, C.c_void_p,
+                          C.POINTER(C.c_uint64)],
 }
 
 _lock = threading.Lock()
@@ -115,7 +132,7 @@ def load(path: str | None = None):
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = C.c_char_p if name == "admm_last_error" else C.c_int
-        if lib.admm_abi_version() != 1:
+        if lib.admm_abi_version() != ABI_VERSION:
             raise AdmmLibraryError("ABI version mismatch")
         if path is None:
             _lib = lib

@@ -71,7 +71,7 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
              max_iters=10, eps_pri=1e-1, eps_dual=1e-1, verbose=True, snapshot_dir=None,
              snapshot_every=None, snapshot_div=10, phantom_true=None, mu=None, tv_iters=10,
              cg_iters=5, tv_kind="iso", group=None, return_tensors=False, timing=None,
-             write_params=True):
+             write_params=True, fusion="midpoint"):
     V_total = len(A_dense_list)
     geom, dtype, device = _common_geometry(A_dense_list)
     if geom.N != N:
@@ -89,7 +89,7 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
     if snapshot_every is None:
         snapshot_every = max(1, max_iters // snapshot_div)  # _ver2:31-32
     nb = NodeBatch(geom, dtype, plan, sinograms, Qij_diag_fn, rho, lam_tv, mu, tv_iters, cg_iters,
-                   tv_kind, phantom_true, device)
+                   tv_kind, phantom_true, device, fusion=fusion, Wi_list=Wi_list)
     halo = HaloExchange(plan, nb.x_ext, group)
     if world > 1:
         dist.barrier(group=group)

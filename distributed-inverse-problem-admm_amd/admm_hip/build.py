@@ -10,7 +10,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(_HERE)
 CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(_HERE, "libadmm_tomo.so")
-SOURCES = ["admm_tomo.hip"]
+SOURCES = ["admm_tomo.hip", "masks.hip"]
 DEPS = SOURCES + ["kernels.hpp"]
 
 

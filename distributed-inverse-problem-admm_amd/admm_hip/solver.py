@@ -40,7 +40,8 @@ def _vec_key(t: torch.Tensor):
 class NodeBatch:
     def __init__(self, geom: ParallelBeamGeometry, dtype: str, plan: ShardPlan, sinograms,
                  Qij_diag_fn, rho: float, lam: float, mu: float, tv_iters: int = 10,
-                 cg_iters: int = 5, tv_kind: str = "iso", phantom=None, device: int = 0):
+                 cg_iters: int = 5, tv_kind: str = "iso", phantom=None, device: int = 0,
+                 fusion: str = "midpoint", Wi_list=None):
         self.lib = _lib.load()
         self.geom = geom
         self.plan = plan
@@ -98,6 +99,18 @@ class NodeBatch:
         self.edge_b = ii(plan.edge_b_row)
         self.y = torch.zeros((max(E, 1), n), dtype=torch.float64, device=dev)
         self.z = torch.zeros((max(E, 1), n), dtype=torch.float64, device=dev)
+        # weighted edge fusion: both endpoint duals + W of every x_ext row
+        if fusion not in ("midpoint", "weighted"):
+            raise ValueError("fusion must be 'midpoint' or 'weighted'")
+        self.fusion = fusion
+        self.y_b = None
+        self.w = None
+        if fusion == "weighted":
+            if Wi_list is None:
+                raise ValueError("weighted fusion needs Wi_list")
+            self.y_b = torch.zeros((max(E, 1), n), dtype=torch.float64, device=dev)
+            self.w = torch.stack([_as_f64_tensor(Wi_list[g], n, dev)
+                                  for g in plan.local_nodes + plan.halo_nodes])
         # D_i = sum_j q_ij  (constant across iterations; setup)
         self.dsum = torch.zeros((V, n), dtype=torch.float64, device=dev)
         for k in range(V):
@@ -115,7 +128,9 @@ class NodeBatch:
             p(self.x_ext), p(self.d), p(self.e), p(self.atb), p(self.dsum), p(self.b), p(self.phantom),
             p(self.y), p(self.z), p(self.q), p(self.edge_a), p(self.edge_b), p(self.inc_off),
             p(self.inc_edge), p(self.inc_qslot), p(self.inc_sign), p(self.node_stats),
-            p(self.edge_stats))
+            p(self.edge_stats),
+            _lib.ADMM_FUSE_WEIGHTED if fusion == "weighted" else _lib.ADMM_FUSE_MIDPOINT, 0,
+            p(self.y_b), p(self.w))
         torch.cuda.synchronize(dev)
         _lib.check(self.lib.admm_batch_bind(self.ctx.h, C.byref(self.cb)), "admm_batch_bind")
         _lib.check(self.lib.admm_batch_atb(self.ctx.h, p(self.atb), C.c_void_p(self._s())),

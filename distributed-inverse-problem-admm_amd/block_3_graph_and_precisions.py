@@ -1,9 +1,84 @@
-"""Drop-in subset of /root/reference/block_3_graph_and_precisions.py.
+"""Drop-in for /root/reference/block_3_graph_and_precisions.py.
 
-``make_precisions(A_dense_list, q_mode)`` (:11-43): W_i[p] = max(||A_i[:,p]||^2,
-1e-12) from the matrix-free HIP kernel, and the arithmetic / harmonic Q_ij
-provider.  The per-pixel kNN / MST / chain masks (:62-319) are not yet ported.
+* ``make_precisions(A_dense_list, q_mode)`` (:11-43): W_i[p] = max(||A_i[:,p]||^2,
+  1e-12) from the matrix-free HIP kernel, and the arithmetic / harmonic Q_ij provider.
+* ``build_pixel_connected_Q_provider(...)`` (:265-319): per-pixel kNN / MST / chain
+  masks from one HIP launch (admm_hip.masks) and the masked Q_ij provider.
+
+Deviation: the reference loads a pickled list of dense matrices from
+``base_dir/A_dense_list_pickle`` (:289-295).  Dense A is infeasible past ~128^2
+and unpickling is not done here: pass ``ops=`` (the RayTransform list of
+``load_odl_data``) or ``Wi_list=`` instead.  ``keep`` comes back as a device
+uint8 tensor [V, V, n] (the reference returns a numpy bool array).
 """
 from __future__ import annotations
 
+import os
+
+import numpy as np
+
 from admm_hip.data import make_precisions  # noqa: F401
+from admm_hip.masks import MaskedQProvider, pixel_masks, union_graph
+
+
+def build_pixel_connected_Q_provider(base_dir="saved_operators_Incmp_Span",
+                                     A_dense_list_pickle="A_dense_list.pkl",
+                                     strategy="knn", k=2, seed=0, q_mode="arithmetic",
+                                     verbose=True, plot_union=True, show_plots=True,
+                                     output_dir="pixel_graphs_out", *, ops=None, Wi_list=None,
+                                     device=None):
+    """Returns (G_union, Wi_list, Qij_diag_masked, keep) like block_3:265-319."""
+    if Wi_list is None:
+        if ops is None:
+            raise FileNotFoundError(
+                f"no operators given: the reference reads {os.path.join(base_dir, A_dense_list_pickle)} "
+                "(pickled dense matrices); pass ops=<RayTransform list> or Wi_list= instead")
+        Wi_list, _ = make_precisions(ops, q_mode=q_mode)
+    if device is None:
+        device = ops[0].device if ops is not None else 0
+    keep = pixel_masks(Wi_list, strategy=strategy, k=k, seed=seed, q_mode=q_mode, device=device)
+    G_union = None
+    if plot_union:
+        tag = f"{strategy}_k{k}_{q_mode}" if strategy == "knn" else f"{strategy}_{q_mode}"
+        G_union = _summarize_union(keep, output_dir, show_plots, verbose, tag)
+    return G_union, Wi_list, MaskedQProvider(Wi_list, keep, q_mode), keep
+
+
+def _summarize_union(keep, output_dir, show_plots, verbose, tag):
+    """Union graph + the diagnostics block_3:190-260 prints and plots."""
+    import networkx as nx
+    G = union_graph(keep)
+    degrees = np.array([d for _, d in G.degree()])
+    active = float(keep.double().mean().item())
+    if verbose:
+        print(f"[Block3] strategy {tag}")
+        print(f"[Block3] nodes {G.number_of_nodes()}, edges {G.number_of_edges()}")
+        print(f"[Block3] connected {nx.is_connected(G)}")
+        if degrees.size:
+            print(f"[Block3] degree min mean max {degrees.min()}  {degrees.mean():.2f}  {degrees.max()}")
+        print(f"[Block3] active pixel ratio {active:.4f}")
+    try:
+        import matplotlib
+        if not show_plots:
+            matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+        os.makedirs(output_dir, exist_ok=True)
+        plt.figure(figsize=(6, 6))
+        nx.draw_networkx(G, pos=nx.spring_layout(G, seed=42), with_labels=True, node_size=600,
+                         font_size=10)
+        plt.tight_layout()
+        plt.savefig(os.path.join(output_dir, f"pixel_union_graph_{tag}.png"), dpi=200)
+        plt.show() if show_plots else plt.close()
+        if degrees.size:
+            plt.figure(figsize=(6, 4))
+            plt.hist(degrees, bins=range(int(degrees.min()), int(degrees.max()) + 2))
+            plt.xlabel("Degree")
+            plt.ylabel("Count")
+            plt.title(f"Node degree histogram, strategy {tag}")
+            plt.tight_layout()
+            plt.savefig(os.path.join(output_dir, f"pixel_union_degree_{tag}.png"), dpi=200)
+            plt.show() if show_plots else plt.close()
+    except Exception as exc:  # plotting is best-effort, as in the reference
+        if verbose:
+            print("[Block3] union graph plot failed:", repr(exc))
+    return G

@@ -8,6 +8,9 @@ updates run on MI355X (admm_hip.admm.run_admm).  Extra keyword arguments:
 * ``cg_iters``  CG steps per round (default 5)
 * ``tv_kind``   "iso" (default) or "aniso"
 * ``group``     torch.distributed process group (default: WORLD if initialised)
+* ``fusion``    "midpoint" (default; z = (a_i + a_j)/2 as the reference runs, :220-223)
+                or "weighted" (z = (W_i a_i + W_j a_j)/(W_i + W_j) with W = Wi_list, the
+                form commented out at :221-222 and ADMM_Algo.pdf eq.(2))
 
 ``max_inner_iters`` is accepted and, as in the reference, unused.
 """
@@ -23,7 +26,7 @@ def decentralized_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn,
                        verbose=True, snapshot_dir=None,
                        snapshot_every=None, snapshot_div=10, phantom_true=None,
                        mu=None, tv_iters=10, cg_iters=5, tv_kind="iso", group=None,
-                       write_params=True):
+                       write_params=True, fusion="midpoint"):
     """Returns (x_list, history) like block_6_admm_loop_ver2.py:310-326."""
     del max_inner_iters  # accepted but unused, as in the reference (_ver2:17)
     return run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=lam_tv, rho=rho,
@@ -31,4 +34,4 @@ def decentralized_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn,
                     snapshot_dir=snapshot_dir, snapshot_every=snapshot_every,
                     snapshot_div=snapshot_div, phantom_true=phantom_true, mu=mu,
                     tv_iters=tv_iters, cg_iters=cg_iters, tv_kind=tv_kind, group=group,
-                    write_params=write_params)
+                    write_params=write_params, fusion=fusion)

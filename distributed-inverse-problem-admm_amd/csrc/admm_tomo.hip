@@ -59,6 +59,11 @@ int ensure(Buf& b, size_t bytes) {
 }
 }  // namespace
 
+// error channel shared with the other translation units (masks.hip)
+namespace admm_internal {
+int fail(int code, const std::string& msg) { return ::fail(code, msg); }
+}  // namespace admm_internal
+
 struct admm_ctx {
   admm_geom g{};
   int dtype = ADMM_DTYPE_F32;
@@ -185,7 +190,8 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
 
   // 1. neighbour gather: c = sum_j q_ij (z_ij - y_ij,i); xs = (T) x (+ transpose)
   hipLaunchKernelGGL((k_gather<T, VB>), tg, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.q, B.inc_off, B.inc_edge,
-                     B.inc_qslot, B.inc_sign, c, xs, xsT, N, V);
+                     B.inc_qslot, B.inc_sign, B.fusion == ADMM_FUSE_WEIGHTED ? B.y_b : nullptr, c, xs, xsT,
+                     N, V);
   CHECK_LAUNCH();
   // 2-4. r = A^T b + rho c + mu K^T(d - e) - H x,  p = r,  rr
   RET((launch_fwd_batch<T, VB, 0>(C, xs, xsT, sino, nullptr, nullptr, V, s)));
@@ -266,6 +272,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
     a.inc_edge = B.inc_edge;
     a.inc_qslot = B.inc_qslot;
     a.inc_sign = B.inc_sign;
+    a.ybv = B.fusion == ADMM_FUSE_WEIGHTED ? B.y_b : nullptr;
     a.rho = B.rho;
     a.lam = B.lam;
     a.mu = B.mu;
@@ -287,8 +294,12 @@ int enqueue_consensus(admm_ctx* C, hipStream_t s) {
   if (B.n_edges == 0) return ADMM_OK;
   const int npix = C->npix;
   dim3 grid((npix + kBlock * 4 - 1) / (kBlock * 4), B.n_edges);
-  hipLaunchKernelGGL(k_consensus, grid, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.edge_a, B.edge_b,
-                     (double*)C->partE.p, npix);
+  if (B.fusion == ADMM_FUSE_WEIGHTED)
+    hipLaunchKernelGGL(k_consensus<true>, grid, dim3(kBlock), 0, s, B.x_ext, B.y, B.y_b, B.z, B.w, B.edge_a,
+                       B.edge_b, (double*)C->partE.p, npix);
+  else
+    hipLaunchKernelGGL(k_consensus<false>, grid, dim3(kBlock), 0, s, B.x_ext, B.y, nullptr, B.z, nullptr,
+                       B.edge_a, B.edge_b, (double*)C->partE.p, npix);
   CHECK_LAUNCH();
   RET(launch_reduce((double*)C->partE.p, 3 * B.n_edges, C->P_edge, B.edge_stats, 1, 1, 0, s));
   return ADMM_OK;
@@ -534,6 +545,9 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   if (B.n_edges > 0 && (!B.y || !B.z || !B.q || !B.edge_a || !B.edge_b || !B.inc_edge || !B.inc_qslot ||
                         !B.inc_sign || !B.edge_stats))
     return fail(ADMM_E_INVALID, "null edge pointer");
+  if (B.fusion != ADMM_FUSE_MIDPOINT && B.fusion != ADMM_FUSE_WEIGHTED) return fail(ADMM_E_INVALID, "bad fusion");
+  if (B.fusion == ADMM_FUSE_WEIGHTED && B.n_edges > 0 && (!B.y_b || !B.w))
+    return fail(ADMM_E_INVALID, "weighted fusion needs y_b and w");
   if (B.n_edges > 65535) return fail(ADMM_E_INVALID, "more than 65535 edge slots on one device");
   const size_t npix = C->npix, m = C->mrays;
   if ((size_t)B.V * npix * 8 >= (1ull << 31) || (size_t)B.V * m * 8 >= (1ull << 31))

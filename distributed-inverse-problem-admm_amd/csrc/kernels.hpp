@@ -541,9 +541,18 @@ struct BackArgs {
   const int* inc_edge;
   const int* inc_qslot;
   const int* inc_sign;
+  const double* ybv;        // DIAG: higher-endpoint duals (weighted fusion) or null
   double rho, lam, mu;
   int tv_kind;
 };
+
+// v_ij = z_ij - y_ij,i seen from the node at incidence sign s (+1 lower endpoint):
+// single-y form y_ij,max = -y when yb is null, else the stored higher-endpoint dual.
+__device__ __forceinline__ double edge_v(const double* __restrict__ z, const double* __restrict__ y,
+                                         const double* __restrict__ yb, int s, size_t eo) {
+  if (yb == nullptr) return z[eo] - (double)s * y[eo];
+  return z[eo] - (s > 0 ? y[eo] : yb[eo]);
+}
 
 // forward difference at (i,j) of a float64 image (zero at the last row / column)
 __device__ __forceinline__ void grad_at(const double* __restrict__ x, int N, int i, int j, double& gx, double& gy) {
@@ -687,7 +696,7 @@ __device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j
       double quad = 0.0;
       for (int q = A.inc_off[v]; q < A.inc_off[v + 1]; ++q) {
         const size_t eo = (size_t)A.inc_edge[q] * npix + pix;
-        const double vij = A.zv[eo] - (double)A.inc_sign[q] * A.yv[eo];
+        const double vij = edge_v(A.zv, A.yv, A.ybv, A.inc_sign[q], eo);
         const double dd = xc - vij;
         quad += A.qv[(size_t)A.inc_qslot[q] * npix + pix] * dd * dd;
       }
@@ -891,7 +900,8 @@ __global__ __launch_bounds__(kBlock) void k_gather(const double* __restrict__ x,
                                                    const double* __restrict__ z, const double* __restrict__ q,
                                                    const int* __restrict__ inc_off, const int* __restrict__ inc_edge,
                                                    const int* __restrict__ inc_qslot,
-                                                   const int* __restrict__ inc_sign, double* __restrict__ c,
+                                                   const int* __restrict__ inc_sign,
+                                                   const double* __restrict__ yb, double* __restrict__ c,
                                                    T* __restrict__ xs, T* __restrict__ xsT, int N, int V) {
   __shared__ TileT<T, VB> tl;
   const EwMap<VB> mp;
@@ -910,7 +920,7 @@ __global__ __launch_bounds__(kBlock) void k_gather(const double* __restrict__ x,
         double acc = 0.0;
         for (int qq = e0; qq < e1; ++qq) {
           const size_t eo = (size_t)inc_edge[qq] * npix + pix;
-          const double vij = z[eo] - (double)inc_sign[qq] * y[eo];
+          const double vij = edge_v(z, y, yb, inc_sign[qq], eo);
           acc += q[(size_t)inc_qslot[qq] * npix + pix] * vij;
         }
         c[(size_t)v * npix + pix] = acc;
@@ -1094,15 +1104,20 @@ __global__ void k_pack(const T* __restrict__ in, T* __restrict__ out, int L, int
 //   a_a = x_a + y, a_b = x_b - y, z' = (a_a + a_b)/2, y' = y + x_a - z'
 //   partials of |x_a - z'|^2, |x_b - z'|^2, |z' - z|^2
 // ===========================================================================
+// WEIGHTED: a_a = x_a + y, a_b = x_b + y_b, z' = (W_a a_a + W_b a_b)/(W_a + W_b),
+//           y' = y + x_a - z', y_b' = y_b + x_b - z'   (_ver2:221-222 commented form, PDF eq.(2))
+template <bool WEIGHTED>
 __global__ __launch_bounds__(kBlock) void k_consensus(const double* __restrict__ xext, double* __restrict__ y,
-                                                      double* __restrict__ z, const int* __restrict__ ea,
-                                                      const int* __restrict__ eb, double* __restrict__ part,
-                                                      int npix) {
+                                                      double* __restrict__ yb, double* __restrict__ z,
+                                                      const double* __restrict__ w,
+                                                      const int* __restrict__ ea, const int* __restrict__ eb,
+                                                      double* __restrict__ part, int npix) {
   __shared__ double lds[12];
   const int e = blockIdx.y;
   const size_t eo = (size_t)e * npix;
-  const double* xa = xext + (size_t)ea[e] * npix;
-  const double* xb = xext + (size_t)eb[e] * npix;
+  const size_t ra_off = (size_t)ea[e] * npix, rb_off = (size_t)eb[e] * npix;
+  const double* xa = xext + ra_off;
+  const double* xb = xext + rb_off;
   double acc[3] = {0.0, 0.0, 0.0};
   const int base = blockIdx.x * (kBlock * 4);
 #pragma unroll
@@ -1110,8 +1125,17 @@ __global__ __launch_bounds__(kBlock) void k_consensus(const double* __restrict__
     const int pix = base + u * kBlock + threadIdx.x;
     if (pix < npix) {
       const double xav = xa[pix], xbv = xb[pix], yv = y[eo + pix], zo = z[eo + pix];
-      const double aa = xav + yv, ab = xbv - yv;
-      const double zn = (aa + ab) * 0.5;
+      double zn;
+      if constexpr (WEIGHTED) {
+        const double ybv = yb[eo + pix];
+        const double wa = w[ra_off + pix], wb = w[rb_off + pix];
+        const double aa = xav + yv, ab = xbv + ybv;
+        zn = (wa * aa + wb * ab) / (wa + wb);
+        yb[eo + pix] = ybv + xbv - zn;
+      } else {
+        const double aa = xav + yv, ab = xbv - yv;
+        zn = (aa + ab) * 0.5;
+      }
       y[eo + pix] = yv + xav - zn;
       z[eo + pix] = zn;
       const double ra = xav - zn, rb = xbv - zn, dz = zn - zo;

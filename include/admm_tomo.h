@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ADMM_ABI_VERSION 1
+#define ADMM_ABI_VERSION 2
 
 #define ADMM_OK 0
 #define ADMM_E_INVALID (-1)
@@ -55,6 +55,11 @@ extern "C" {
 
 #define ADMM_TV_ISO 0
 #define ADMM_TV_ANISO 1
+
+/* edge fusion (admm_batch.fusion) */
+#define ADMM_FUSE_MIDPOINT 0 /* z = (a_i + a_j)/2   (block_6_admm_loop_ver2.py:220-223, as run) */
+#define ADMM_FUSE_WEIGHTED 1 /* z = (W_i a_i + W_j a_j)/(W_i + W_j)  (commented at _ver2:221-222;
+                                ADMM_Algo.pdf eq.(2)); keeps both endpoint duals */
 
 /* per-node statistics written by admm_node_update (float64) */
 #define ADMM_NODE_STAT_MSE_SINO 0 /* ||A x - b||^2           (block_6_admm_loop_ver2.py:190-194) */
@@ -116,6 +121,13 @@ typedef struct admm_batch {
 
     double* node_stats;   /* [V][ADMM_NODE_STATS] */
     double* edge_stats;   /* [E][ADMM_EDGE_STATS] */
+
+    /* ABI 2: edge fusion.  MIDPOINT keeps the single-y form (y_ij,max = -y);
+     * WEIGHTED needs y_b and w (both NULL for MIDPOINT). */
+    int32_t fusion;       /* ADMM_FUSE_* */
+    int32_t reserved2;
+    double* y_b;          /* [E][n] dual of the higher-numbered endpoint (y_ij,max)   */
+    const double* w;      /* [n_xext][n] W of the node in each x_ext row (W_i, make_precisions) */
 } admm_batch;
 
 int admm_abi_version(void);
@@ -149,11 +161,13 @@ int admm_tv_div(admm_ctx* ctx, const double* px, const double* py, double* out, 
 int admm_batch_bind(admm_ctx* ctx, const admm_batch* batch);
 /* A^T b for the bound batch (setup; writes batch->atb, which is then const). */
 int admm_batch_atb(admm_ctx* ctx, double* atb_out, void* stream);
-/* One x-update of every bound node: neighbour gather v_ij = z_ij - y_ij,i,
+/* One x-update of every bound node: neighbour gather v_ij = z_ij - y_ij,i
+ * (y_ij,i = y for the lower endpoint, -y or y_b for the higher one),
  * fixed-count split-Bregman/CG solve of eq.(1), diagnostics into node_stats.
  * Replaces block_6_admm_loop_ver2.py:81-197 (build_node_problem + SCS + g check). */
 int admm_node_update(admm_ctx* ctx, void* stream);
-/* Edge updates z = (a_i + a_j)/2, y += x - z and the residual partial sums
+/* Edge updates z = (a_i + a_j)/2 (or the W-weighted mean, ADMM_FUSE_WEIGHTED),
+ * y += x - z at both ends, and the residual partial sums
  * into edge_stats.  Replaces block_6_admm_loop_ver2.py:210-253.  Every edge
  * slot of the batch is processed; x_ext halo rows must be current. */
 int admm_consensus(admm_ctx* ctx, void* stream);
@@ -161,6 +175,33 @@ int admm_consensus(admm_ctx* ctx, void* stream);
  * projector on the bound batch's current x, timed with HIP events on `stream`.
  * Measurement helper for bench.py; synchronises. */
 int admm_time_forward(admm_ctx* ctx, int reps, void* stream, double* ms_out);
+
+/* --- per-pixel edge masks for masked precisions (setup) --- */
+
+#define ADMM_MASK_KNN 0   /* top-k per node, symmetrised, + max spanning tree if disconnected */
+#define ADMM_MASK_MST 1   /* maximum spanning tree of the complete graph at the pixel        */
+#define ADMM_MASK_CHAIN 2 /* random permutation chain (orders from admm_chain_orders)         */
+#define ADMM_Q_ARITHMETIC 0 /* q_ij = max((W_i + W_j)/2, 1e-12)        (block_3:33-39) */
+#define ADMM_Q_HARMONIC 1   /* q_ij = max(W_i W_j / (W_i + W_j), 1e-12) (block_3:26-32) */
+#define ADMM_MASK_MAX_NODES 64
+
+/* keep[(i*V + j)*n + p] = 1 if edge (i, j) is active at pixel p, for all ordered pairs
+ * (symmetric, zero diagonal).  Replaces _build_all_pixel_masks and its per-pixel helpers
+ * (block_3_graph_and_precisions.py:62-187: _pixel_mask_knn_then_connect :62-110,
+ * _pixel_mask_mst :113-131, _pixel_mask_chain :134-151).  W: [V][n] float64 device
+ * (make_precisions' W_i), orders: [n][V] int32 device (ADMM_MASK_CHAIN only, else NULL),
+ * keep: [V][V][n] uint8 device.  2 <= V <= ADMM_MASK_MAX_NODES.  kNN ties (equal q) go to
+ * the higher node index; the reference's tie order is numpy argpartition's (unspecified).
+ * Asynchronous on `stream` (current device). */
+int admm_pixel_masks(const double* W, int V, int64_t n, int strategy, int k, int q_mode,
+                     const int32_t* orders, uint8_t* keep, void* stream);
+/* Host: the node orders of `_pixel_mask_chain` (block_3:134-151) for n pixels --
+ * numpy Generator(PCG64).permutation(V) called n times in pixel order, replayed from
+ * the bit generator state {state, inc} (pcg[0..3] = state_hi, state_lo, inc_hi, inc_lo;
+ * has_uint32 / uinteger as numpy reports them).  orders: [n][V] int32 host memory.
+ * pcg_out (may be NULL) receives the state afterwards (same layout + has_uint32, uinteger). */
+int admm_chain_orders(const uint64_t pcg[4], int has_uint32, uint32_t uinteger, int V, int64_t n,
+                      int32_t* orders, uint64_t pcg_out[6]);
 
 #ifdef __cplusplus
 }

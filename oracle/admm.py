@@ -7,6 +7,8 @@ of ``node_solver`` (fixed-count split-Bregman + CG instead of CVXPY+SCS):
   * neighbour gather v_ij = z_ij - y_ij,i, q_ij = Qij_diag_fn(i,j) (:85-95)
   * eps_target = 2/(k+1)^1.005, first SCS eps = min(1e-2, eps_target) (:101-108)
   * z_ij = (a_i + a_j)/2 with a = x + y (:210-223); y += x - z (:225-230)
+  * fusion="weighted": z_ij = (W_i a_i + W_j a_j)/(W_i + W_j), the form the
+    code comments at :216-222 and ADMM_Algo.pdf eq.(2) give
   * r2, s2, per-node attribution, sqrt, stop test (:232-289)
   * history keys (:310-326)
 
@@ -15,7 +17,10 @@ the lower-numbered endpoint a, the other endpoint's dual is -y_e (with y0=0,
 y_ij,i + y_ij,j = 0 holds after every update -- SURVEY.md 8a row a7).  Both
 ends then evaluate  a_a = x_a + y_e,  a_b = x_b - y_e,  z = (a_a + a_b)/2,
 y_e += x_a - z  in that order.  ``edge_update_literal`` restates the
-reference's two-dual dict form verbatim for cross-checking.
+reference's two-dual dict form verbatim for cross-checking.  Weighted fusion
+breaks y_ij,i + y_ij,j = 0, so it keeps both duals: y_e (lower endpoint a) and
+y2_e (higher endpoint b):  a_a = x_a + y_e,  a_b = x_b + y2_e,
+z = (W_a a_a + W_b a_b)/(W_a + W_b),  y_e += x_a - z,  y2_e += x_b - z.
 """
 from __future__ import annotations
 
@@ -41,14 +46,22 @@ def eps_target(k: int) -> float:
     return 2.0 / ((k + 1) ** 1.005)  # block_6_admm_loop_ver2.py:101-103
 
 
-def edge_update_literal(G, x, y, z):
-    """Verbatim restatement of block_6_admm_loop_ver2.py:210-230 (two duals per edge)."""
+def edge_update_literal(G, x, y, z, Wi_list=None):
+    """Verbatim restatement of block_6_admm_loop_ver2.py:210-230 (two duals per edge).
+
+    With ``Wi_list`` the numerator/denominator are the weighted ones the
+    reference leaves commented out at :221-222.
+    """
     new_z = {}
     for i, j in G.edges():
         key = (min(i, j), max(i, j))
         a_i = x[i] + y[(key[0], key[1], i)]
         a_j = x[j] + y[(key[0], key[1], j)]
-        new_z[key] = (a_i + a_j) / 2.0
+        if Wi_list is None:
+            new_z[key] = (a_i + a_j) / 2.0
+        else:
+            Wi, Wj = Wi_list[i], Wi_list[j]
+            new_z[key] = (Wi * a_i + Wj * a_j) / (Wi + Wj)
     new_y = {}
     for i, j in G.edges():
         key = (min(i, j), max(i, j))
@@ -60,13 +73,20 @@ def edge_update_literal(G, x, y, z):
 def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
                        max_iters=10, eps_pri=1e-1, eps_dual=1e-1, phantom_true=None,
                        mu=None, tv_iters=10, cg_iters=5, tv_kind="iso",
-                       dtype=np.float64, node_subset=None):
+                       dtype=np.float64, node_subset=None, fusion="midpoint", Wi_list=None):
     """Oracle ADMM.  ``ops`` = list of scipy sparse matrices (one per node).
 
     Returns (x_list, history) with the reference's history keys.  With
     ``node_subset`` only those nodes' x-updates run (the others keep x=0); used
-    only to time a bounded CPU sample.
+    only to time a bounded CPU sample.  ``fusion="weighted"`` needs ``Wi_list``.
     """
+    if fusion not in ("midpoint", "weighted"):
+        raise ValueError("fusion must be 'midpoint' or 'weighted'")
+    weighted = fusion == "weighted"
+    if weighted:
+        if Wi_list is None:
+            raise ValueError("weighted fusion needs Wi_list")
+        W = [np.asarray(w, dtype=np.float64).reshape(-1) for w in Wi_list]
     V = len(ops)
     n = N * N
     mu = (10.0 * lam_tv if mu is None else mu)
@@ -79,6 +99,7 @@ def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
     states = [ns.NodeState.zeros(n, dtype) for _ in range(V)]
     y = {e: np.zeros(n) for e in edges}
     z = {e: np.zeros(n) for e in edges}
+    y2 = {e: np.zeros(n) for e in edges} if weighted else None
     nbrs = {i: list(G.neighbors(i)) for i in range(V)}
     hist = {k: [] for k in HISTORY_KEYS}
     ph = None
@@ -97,7 +118,7 @@ def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
             c = np.zeros(n)
             for j in nbrs[i]:
                 e = (min(i, j), max(i, j))
-                yi = y[e] if i == e[0] else -y[e]
+                yi = y[e] if i == e[0] else (y2[e] if weighted else -y[e])
                 v = z[e] - yi
                 q = np.asarray(Qij_diag_fn(i, j), dtype=np.float64)
                 D += q
@@ -127,8 +148,13 @@ def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
         for (a_, b_) in edges:
             e = (a_, b_)
             aa = x[a_] + y[e]
-            ab = x[b_] - y[e]
-            zn = (aa + ab) * 0.5
+            if weighted:
+                ab = x[b_] + y2[e]
+                zn = (W[a_] * aa + W[b_] * ab) / (W[a_] + W[b_])
+                y2[e] = y2[e] + x[b_] - zn
+            else:
+                ab = x[b_] - y[e]
+                zn = (aa + ab) * 0.5
             y[e] = y[e] + x[a_] - zn
             ra = x[a_] - zn
             rb = x[b_] - zn

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
         assert name in _lib.SYMBOLS, f"{name} not bound in _lib.SYMBOLS"
     assert set(_lib.SYMBOLS) == set(names)
-    assert lib.admm_abi_version() == 1
+    assert lib.admm_abi_version() == _lib.ABI_VERSION == 2
 
 
 def test_error_path_without_gpu_work():
@@ -88,6 +88,10 @@ REF_SIGNATURES = {
         "save_operators_dir", "build_dense"],
     # /root/reference/block_3_graph_and_precisions.py:11
     ("block_3_graph_and_precisions", "make_precisions"): ["ops", "q_mode"],
+    # /root/reference/block_3_graph_and_precisions.py:265-274
+    ("block_3_graph_and_precisions", "build_pixel_connected_Q_provider"): [
+        "base_dir", "A_dense_list_pickle", "strategy", "k", "seed", "q_mode", "verbose", "plot_union",
+        "show_plots", "output_dir"],
 }
 REF_DEFAULTS = {
     ("block_6_admm_loop_ver2", "decentralized_admm"): dict(lam_tv=0.01, rho=1.0, max_iters=10,

@@ -38,16 +38,31 @@ def setup_problem(N, V, angles_total, dtype="float32", seed=1000):
     return ops, ph.numpy(), sinos, Wi, Q, A, sin_h
 
 
+def node_weights(Wi, seed=5):
+    """Per-node, per-pixel distinct W_i (all nodes share one geometry, so the
+    make_precisions W_i are identical and weighted fusion would equal the midpoint)."""
+    rng = np.random.default_rng(seed)
+    W = [np.asarray(w.double().cpu().numpy() if hasattr(w, "cpu") else w, dtype=np.float64)
+         * np.exp(0.7 * rng.standard_normal(np.asarray(w.shape).prod())) for w in Wi]
+    Q = lambda i, j: np.maximum(0.5 * (W[i] + W[j]), 1e-12)  # noqa: E731  block_3:33-39
+    return W, Q
+
+
 def compare(G, N, V, iters, angles_total, dtype="float32", tol=1e-5, tv_kind="iso", lam=0.02,
-            rho=2.0, tv_iters=10, cg_iters=5):
+            rho=2.0, tv_iters=10, cg_iters=5, fusion="midpoint"):
     ops, ph, sinos, Wi, Q, A, sin_h = setup_problem(N, V, angles_total, dtype)
+    Wo = None
+    if fusion == "weighted":
+        Wi, Q = node_weights(Wi)
+        Wo = Wi
     x, h = decentralized_admm(ops, sinos, G, Wi, Q, N, lam_tv=lam, rho=rho, max_iters=iters,
                               eps_pri=0.0, eps_dual=0.0, verbose=False, phantom_true=ph,
                               tv_kind=tv_kind, tv_iters=tv_iters, cg_iters=cg_iters,
-                              write_params=False)
+                              write_params=False, fusion=fusion)
     xo, ho = oadmm.decentralized_admm([A] * V, sin_h, G, Q, N, lam_tv=lam, rho=rho,
                                       max_iters=iters, eps_pri=0.0, eps_dual=0.0, phantom_true=ph,
-                                      tv_kind=tv_kind, tv_iters=tv_iters, cg_iters=cg_iters)
+                                      tv_kind=tv_kind, tv_iters=tv_iters, cg_iters=cg_iters,
+                                      fusion=fusion, Wi_list=Wo)
     assert set(h) >= set(oadmm.HISTORY_KEYS)
     errs = {"x": rel(np.stack(x), np.stack(xo))}
     for k in ("primal", "dual"):
@@ -81,9 +96,28 @@ def test_complete_graph_anisotropic_matches_oracle(cuda):
     compare(nx.complete_graph(5), 32, 5, 6, 100, tv_kind="aniso")
 
 
+def test_weighted_fusion_matches_oracle(cuda):
+    """z = (W_i a_i + W_j a_j)/(W_i + W_j), both endpoint duals."""
+    x, h, xo, ho = compare(nx.cycle_graph(4), 48, 4, 10, 192, fusion="weighted")
+    # the weighted run differs from the midpoint one (the weights matter)
+    xm, hm, _, _ = compare(nx.cycle_graph(4), 48, 4, 10, 192)
+    assert rel(h["primal"], hm["primal"]) > 1e-3
+
+
+def test_weighted_fusion_er_graph_float64(cuda):
+    seed = next(s for s in range(100) if nx.is_connected(nx.erdos_renyi_graph(5, 0.6, seed=s)))
+    compare(nx.erdos_renyi_graph(5, 0.6, seed=seed), 24, 5, 5, 80, dtype="float64", tol=1e-9,
+            fusion="weighted", tv_kind="aniso")
+
+
 def test_float64_samples_tight(cuda):
     """C5 arithmetic (float64 samples): agreement to 1e-9."""
     compare(nx.cycle_graph(3), 32, 3, 6, 96, dtype="float64", tol=1e-9)
+
+
+def test_float64_eight_nodes_per_chunk(cuda):
+    """float64 samples with V=8 on one device: the 8-wide node chunk (largest LDS windows)."""
+    compare(nx.cycle_graph(8), 32, 8, 4, 96, dtype="float64", tol=1e-9)
 
 
 def test_odd_tv_rounds_and_single_cg(cuda):

@@ -224,6 +224,52 @@ def test_single_y_form_equals_reference_two_dual_form():
             assert np.allclose(z1[e], 0.5 * (x[e[0]] + x[e[1]]), atol=1e-13)
 
 
+def test_weighted_two_dual_form_equals_reference_weighted_form():
+    """Weighted fusion (commented form _ver2:221-222): the oracle's (y, y2) edge state
+    reproduces the literal two-dual dict update; y_ij,i + y_ij,j = 0 no longer holds."""
+    rng = np.random.default_rng(11)
+    G = nx.Graph([(0, 1), (2, 1), (2, 0), (3, 2)])
+    n = 40
+    W = [np.exp(rng.standard_normal(n)) for _ in range(4)]
+    y_lit = {}
+    for i, j in G.edges():
+        key = (min(i, j), max(i, j))
+        y_lit[(key[0], key[1], i)] = np.zeros(n)
+        y_lit[(key[0], key[1], j)] = np.zeros(n)
+    z_lit = {(min(i, j), max(i, j)): np.zeros(n) for i, j in G.edges()}
+    y1 = {e: np.zeros(n) for e in z_lit}
+    y2 = {e: np.zeros(n) for e in z_lit}
+    for _ in range(4):
+        x = [rng.standard_normal(n) for _ in range(4)]
+        z_lit, y_lit = oadmm.edge_update_literal(G, x, y_lit, z_lit, Wi_list=W)
+        for (a, b) in oadmm.canonical_edges(G):
+            e = (a, b)
+            aa, ab = x[a] + y1[e], x[b] + y2[e]
+            zn = (W[a] * aa + W[b] * ab) / (W[a] + W[b])
+            y1[e] = y1[e] + x[a] - zn
+            y2[e] = y2[e] + x[b] - zn
+            assert np.array_equal(zn, z_lit[e])  # IEEE + is commutative: orientation-free
+            assert np.array_equal(y1[e], y_lit[(a, b, a)]) and np.array_equal(y2[e], y_lit[(a, b, b)])
+    e = (0, 1)
+    assert np.abs(y1[e] + y2[e]).max() > 1e-3
+
+
+def test_weighted_fusion_with_equal_weights_is_midpoint():
+    A = joseph_matrix(Geometry(10, 8))
+    W = np.maximum(np.asarray(A.multiply(A).sum(axis=0)).ravel(), 1e-12)
+    ph = shepp_logan(10, 2).ravel()
+    sinos = [A @ ph + 0.01 * np.random.default_rng(i).standard_normal(A.shape[0]) for i in range(3)]
+    kw = dict(lam_tv=0.02, rho=2.0, max_iters=3, eps_pri=0.0, eps_dual=0.0, tv_iters=2, cg_iters=2)
+    G = nx.cycle_graph(3)
+    xm, hm = oadmm.decentralized_admm([A] * 3, sinos, G, lambda i, j: W, 10, **kw)
+    xw, hw = oadmm.decentralized_admm([A] * 3, sinos, G, lambda i, j: W, 10, fusion="weighted",
+                                      Wi_list=[W] * 3, **kw)
+    assert rel(np.stack(xw), np.stack(xm)) < 1e-13
+    assert np.allclose(hw["primal"], hm["primal"], rtol=1e-12)
+    with pytest.raises(ValueError):
+        oadmm.decentralized_admm([A] * 3, sinos, G, lambda i, j: W, 10, fusion="weighted", **kw)
+
+
 def test_eps_target_and_stop_rule():
     assert oadmm.eps_target(0) == 2.0
     assert abs(oadmm.eps_target(9) - 2.0 / 10 ** 1.005) < 1e-15
