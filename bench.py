@@ -80,6 +80,22 @@ def cpu_baseline(seconds_budget=20.0):
                       f"{el:.1f} s timed, {build_s:.1f} s matrix build excluded"}
 
 
+# HBM bytes per forward-projector launch from the committed rocprofv3 PMC summary
+# (scripts/pmc.sh + scripts/traffic_summary.py; 2 x FETCH_SIZE + WRITE_SIZE per the
+# MI355X_MICROARCH.md gfx950 correction).  PMC counters cannot be read inside this run.
+TRAFFIC_FILE = "profiles/r1_traffic.json"
+FWD_KERNELS = ("admm::k_fwdg<float, 8>", "admm::k_fwd_combine<float, 8, 0>")
+
+
+def pmc_traffic(names):
+    try:
+        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), TRAFFIC_FILE)) as f:
+            k = json.load(f)["kernels"]
+        return float(sum(k[n]["hbm_bytes_per_launch"] for n in names))
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -154,6 +170,7 @@ def main():
     fwd_ms = nb.time_forward(args.fwd_reps)
     B_A, B_At, B_node = node_bytes(N_IMG, ANGLES_PER_NODE, TV_ITERS, CG_ITERS)
     achieved = B_A * plan.V / (fwd_ms * 1e-3) / 1e9
+    fwd_traffic = pmc_traffic(FWD_KERNELS)
     result = {
         "metric": "ADMM node-updates/sec (whole node), 512² phantom; rel-Fro vs CPU ref",
         "value": value,
@@ -181,7 +198,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": fwd_traffic,
+            "traffic_source": TRAFFIC_FILE if fwd_traffic is not None else None,
             "avg_launch_ms": fwd_ms,
             "bytes_per_launch": B_A * plan.V,
             "note": "sample-touch bytes (SURVEY 8d); image/sinogram are L2/MALL resident, so frac>1 "

@@ -731,26 +731,29 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
   const int N = A.N, n_det = A.n_det, n_ang = A.n_ang;
   const int m_rays = n_ang * n_det;
   const int jb = blockIdx.x * kBTJ, ib = blockIdx.y * kBTI;
-  const int j = jb + (threadIdx.x & 63);
-  const int i = ib + (threadIdx.x >> 6);
+  // each wave covers a 16 (j) x 4 (i) patch: a 16-lane ds_read_b128 group then spans
+  // <= ~16 detector bins for any angle (64 x 1 rows spanned up to 27 -> bank conflicts)
+  const int lane = threadIdx.x & 63;
+  const int j = jb + 16 * (threadIdx.x >> 6) + (lane & 15);
+  const int i = ib + (lane >> 4);
   const bool inb = (i < N) && (j < N);
   const int chunk = blockIdx.z;
   const int v0 = chunk * VB;
   const int nv = (MODE == BACK_WSQ) ? 1 : min(VB, A.V - v0);
-  // geometry uses clamped coordinates so out-of-image threads stay inside the window
+  // geometry uses clamped coordinates so out-of-image threads stay inside the window;
+  // the angle constants are uniform -> scalar loads (shared table, scalar-cache resident)
   const double djc = (double)min(j, N - 1), dic = (double)min(i, N - 1);
   const int jhi = min(jb + kBTJ - 1, N - 1), ihi = min(ib + kBTI - 1, N - 1);
 
   __shared__ Pack<T, PV> win[NPL][(MODE == BACK_WSQ) ? 1 : kBAngC][kBWin];
-  __shared__ BackAngle sang[kBAngC];
   __shared__ int kmin_s[kBAngC];
   T acc[VB];
 #pragma unroll
   for (int u = 0; u < VB; ++u) acc[u] = T(0);
   const T* sino_c = A.sino + (size_t)chunk * m_rays * VB;
 
-  auto tap = [&](int tt, T& w0, T& w1, Pack<T, PV> (&s0)[NPL], Pack<T, PV> (&s1)[NPL]) {
-    const BackAngle g = sang[tt];
+  auto tap = [&](int t, int tt, T& w0, T& w1, Pack<T, PV> (&s0)[NPL], Pack<T, PV> (&s1)[NPL]) {
+    const BackAngle g = A.ang[t];
     const double kf = fma(dic, g.Bi, fma(djc, g.Bj, g.B0));
     const double kfl = floor(kf);
     const int k0 = (int)kfl;
@@ -786,18 +789,17 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
 
   for (int t0 = 0; t0 < n_ang; t0 += kBAngC) {
     const int nt = min(kBAngC, n_ang - t0);
-    __syncthreads();
-    if ((int)threadIdx.x < nt) {
-      const BackAngle g = A.ang[t0 + threadIdx.x];
-      sang[threadIdx.x] = g;
-      const double k00 = fma((double)ib, g.Bi, fma((double)jb, g.Bj, g.B0));
-      const double k01 = fma((double)ib, g.Bi, fma((double)jhi, g.Bj, g.B0));
-      const double k10 = fma((double)ihi, g.Bi, fma((double)jb, g.Bj, g.B0));
-      const double k11 = fma((double)ihi, g.Bi, fma((double)jhi, g.Bj, g.B0));
-      kmin_s[threadIdx.x] = (int)floor(fmin(fmin(k00, k01), fmin(k10, k11))) - 1;
-    }
-    __syncthreads();
     if constexpr (MODE != BACK_WSQ) {
+      __syncthreads();
+      if ((int)threadIdx.x < nt) {
+        const BackAngle g = A.ang[t0 + threadIdx.x];
+        const double k00 = fma((double)ib, g.Bi, fma((double)jb, g.Bj, g.B0));
+        const double k01 = fma((double)ib, g.Bi, fma((double)jhi, g.Bj, g.B0));
+        const double k10 = fma((double)ihi, g.Bi, fma((double)jb, g.Bj, g.B0));
+        const double k11 = fma((double)ihi, g.Bi, fma((double)jhi, g.Bj, g.B0));
+        kmin_s[threadIdx.x] = (int)floor(fmin(fmin(k00, k01), fmin(k10, k11))) - 1;
+      }
+      __syncthreads();
       for (int q = threadIdx.x; q < nt * kBWin * NPL; q += kBlock) {
         const int pl = q % NPL, aw = q / NPL;
         const int a = aw / kBWin, w = aw - a * kBWin;
@@ -817,15 +819,15 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
     for (; tt + 1 < nt; tt += 2) {
       T wa0, wa1, wb0, wb1;
       Pack<T, PV> sa0[NPL], sa1[NPL], sb0[NPL], sb1[NPL];
-      tap(tt, wa0, wa1, sa0, sa1);
-      tap(tt + 1, wb0, wb1, sb0, sb1);
+      tap(t0 + tt, tt, wa0, wa1, sa0, sa1);
+      tap(t0 + tt + 1, tt + 1, wb0, wb1, sb0, sb1);
       fmac(wa0, wa1, sa0, sa1);
       fmac(wb0, wb1, sb0, sb1);
     }
     if (tt < nt) {
       T wa0, wa1;
       Pack<T, PV> sa0[NPL], sa1[NPL];
-      tap(tt, wa0, wa1, sa0, sa1);
+      tap(t0 + tt, tt, wa0, wa1, sa0, sa1);
       fmac(wa0, wa1, sa0, sa1);
     }
   }
