@@ -30,18 +30,22 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, out: str | None = None,
+          defines: dict | None = None) -> str:
+    """Build the library (``out``/``defines``: tuning variants for sweeps, never the default)."""
+    target = out or OUT
+    if not force and out is None and not needs_build():
         return OUT
     arch = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
-    tmp = OUT + ".tmp"
+    tmp = target + ".tmp"
+    dflags = [f"-D{k}={v}" for k, v in (defines or {}).items()]
     cmd = [hipcc(), f"--offload-arch={arch}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+           "-Wall", "-Wno-unused-function", *dflags, "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, target)
+    return target
 
 
 if __name__ == "__main__":

@@ -72,6 +72,8 @@ struct admm_ctx {
   int npix = 0, mrays = 0;
   FwdAngle* fang = nullptr;
   BackAngle* bang = nullptr;
+  BackAngleC* bangc = nullptr;
+  double Kb = 0.0;  // angle-independent part of the back projector's k_f
   FgGroup* groups = nullptr;  // angle groups of the grouped forward projector
   int n_groups = 0;           // 0: geometry does not fit the grouped kernel -> k_fwd
   hipStream_t cap = nullptr;  // private capture stream
@@ -141,6 +143,8 @@ int launch_fwd_batch(admm_ctx* C, const T* img, const T* imgT, T* sino, const T*
 template <typename T, int VB, int MODE>
 int launch_back(admm_ctx* C, BackArgs<T> a, int V, hipStream_t s) {
   a.ang = C->bang;
+  a.angc = C->bangc;
+  a.K = C->Kb;
   a.N = C->g.N;
   a.n_det = C->g.n_det;
   a.n_ang = C->g.n_angles;
@@ -374,6 +378,8 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
   // geometry tables, float64 (oracle/geometry.py)
   std::vector<FwdAngle> fa(g.n_angles);
   std::vector<BackAngle> ba(g.n_angles);
+  std::vector<BackAngleC> bc(g.n_angles);
+  C->Kb = -g.det_min / hd - 0.5;
   const double c0 = 0.5 * (g.N - 1);
   for (int t = 0; t < g.n_angles; ++t) {
     const double th = g.angle_min + (t + 0.5) * (g.angle_max - g.angle_min) / g.n_angles;
@@ -390,6 +396,12 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
     ba[t].B0 = -c0 * (ba[t].Bi + ba[t].Bj) - g.det_min / hd - 0.5;
     ba[t].slope = (hd / h) / std::fabs(al);
     ba[t].L = h / std::fabs(al);
+    bc[t].Bi = ba[t].Bi;
+    bc[t].Bj = ba[t].Bj;
+    bc[t].sLf = (float)(ba[t].slope * ba[t].L);
+    bc[t].Lf = (float)ba[t].L;
+    bc[t].LmsLf = (float)(ba[t].L - ba[t].slope * ba[t].L);
+    bc[t].pad = 0.f;
   }
   // angle groups for the grouped forward projector: consecutive angles of one case,
   // G <= 4, such that the union row window of a 64-ray chunk fits kFgWin (float64,
@@ -436,6 +448,8 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
   }
   HIPCHK(hipMemcpy(C->fang, fa.data(), fa.size() * sizeof(FwdAngle), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(C->bang, ba.data(), ba.size() * sizeof(BackAngle), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&C->bangc, bc.size() * sizeof(BackAngleC)));
+  HIPCHK(hipMemcpy(C->bangc, bc.data(), bc.size() * sizeof(BackAngleC), hipMemcpyHostToDevice));
   if (fits && !groups.empty()) {
     HIPCHK(hipMalloc(&C->groups, groups.size() * sizeof(FgGroup)));
     HIPCHK(hipMemcpy(C->groups, groups.data(), groups.size() * sizeof(FgGroup), hipMemcpyHostToDevice));
@@ -457,6 +471,7 @@ int admm_ctx_destroy(admm_ctx* C) {
     if (b->p) (void)hipFree(b->p);
   if (C->fang) (void)hipFree(C->fang);
   if (C->bang) (void)hipFree(C->bang);
+  if (C->bangc) (void)hipFree(C->bangc);
   if (C->groups) (void)hipFree(C->groups);
   if (C->cap) (void)hipStreamDestroy(C->cap);
   delete C;

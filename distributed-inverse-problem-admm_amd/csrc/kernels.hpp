@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace admm {
 
 constexpr int kBlock = 256;
@@ -46,6 +48,14 @@ struct FwdAngle {
 struct BackAngle {
   double B0, Bi, Bj;
   double slope, L;
+};
+
+// Compact per-angle record of the back projector's hot loop (one s_load_dwordx8):
+// k_f = (i - c0) Bi + (j - c0) Bj + K with K = -det_min/hd - 1/2 the same for every
+// angle; float32 weights w0 = max(0, L - f sL), w1 = max(0, (L - sL) + f sL).
+struct alignas(32) BackAngleC {
+  double Bi, Bj;
+  float sLf, Lf, LmsLf, pad;
 };
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
@@ -340,10 +350,36 @@ __global__ __launch_bounds__(kFwdBlock) void k_fwd(const T* __restrict__ img, co
 // and taps run at LDS rate.  The host sizes groups so the window fits
 // (FgGroup tables; wider N -> smaller G).  Segment partial sums go to
 // part[seg][chunk][ray][VB] and k_fwd_combine adds them in fixed order.
+//
+// LDS bank conflicts.  Adjacent rays sit A1 in [1, 1.41] pixels apart, so a
+// ds_read_b128 lane group of 16 rays spans up to ~23 pixels and, with one 16-B
+// slot per pixel, wraps the 16 slots of the bank space (2-3-way conflicts).
+// Each staged row is therefore split into its even and odd pixels (two
+// half-windows, the odd one 64 B further so 8-lane staging writes stay
+// conflict-free): a ray's taps {p, p+1} are one even and one odd pixel, the two
+// reads of a row are "every lane's even tap" and "every lane's odd tap", and a
+// 16-ray group needs <= 12 distinct slots of each.  Lanes are permuted so each
+// hardware lane group ({0-3,12-15,20-27}, ...) holds 16 consecutive rays.
 // ===========================================================================
-constexpr int kFgRows = 8;
+#ifndef ADMM_FG_ROWS
+#define ADMM_FG_ROWS 4
+#endif
+#ifndef ADMM_FG_SEG
+#define ADMM_FG_SEG 8
+#endif
+constexpr int kFgRows = ADMM_FG_ROWS;  // rows staged per LDS chunk
 constexpr int kFgWin = 160;
-constexpr int kFgSeg = 4;
+constexpr int kFgSeg = ADMM_FG_SEG;    // row segments (partial sums) per ray
+constexpr int kFgHalf = kFgWin / 2;        // slots per parity
+constexpr int kFgOdd = kFgHalf + 4;        // odd half-window offset (+64 B bank shift)
+constexpr int kFgRow = kFgOdd + kFgHalf;   // 16-B slots per staged row and plane
+
+// ray (within a 64-ray chunk) of each lane: ds_read_b128 lane groups -> 16 consecutive rays
+__device__ __forceinline__ int fg_ray_of_lane(int lane) {
+  const int l = lane & 31;
+  const int r = l < 4 ? l : l < 12 ? l + 12 : l < 16 ? l - 8 : l < 20 ? l + 8 : l < 28 ? l - 12 : l;
+  return (lane & 32) + r;
+}
 
 struct FgGroup {
   int t0, G;
@@ -361,7 +397,7 @@ __global__ __launch_bounds__(kBlock) void k_fwdg(const T* __restrict__ img, cons
   const FgGroup gr = groups[blockIdx.y];
   const int seg = blockIdx.z % kFgSeg, chunk = blockIdx.z / kFgSeg;
   const int npix = N * N;
-  const int k = kc * 64 + lane;
+  const int k = kc * 64 + fg_ray_of_lane(lane);
   const int kcl = min(k, n_det - 1);
   const int t = gr.t0 + min(g, gr.G - 1);
   const FwdAngle a = ang[t];
@@ -371,7 +407,7 @@ __global__ __launch_bounds__(kBlock) void k_fwdg(const T* __restrict__ img, cons
   const int m_lo = seg * N / kFgSeg, m_hi = (seg + 1) * N / kFgSeg;
   const int nrows = m_hi - m_lo;
 
-  __shared__ Pack<T, PV> win[NPL][kFgRows][kFgWin];
+  __shared__ Pack<T, PV> win[NPL][kFgRows][kFgRow];
   __shared__ int wlo_s[(4096 + kFgSeg - 1) / kFgSeg];  // every row window of the segment (N <= 4096)
   for (int r = threadIdx.x; r < nrows; r += kBlock) {
     const double dm = (double)(m_lo + r);
@@ -411,11 +447,15 @@ __global__ __launch_bounds__(kBlock) void k_fwdg(const T* __restrict__ img, cons
       if (q < kFgRows * kFgWin * NPL) {
         const int pl = q % NPL, rw = q / NPL;
         const int r = rw / kFgWin, w = rw - r * kFgWin;
-        win[pl][r][w] = stage[e];
+        win[pl][r][(w & 1) ? kFgOdd + (w >> 1) : (w >> 1)] = stage[e];
       }
     }
   };
 
+  // float samples: ray position l = l0 + m dl advanced per row in 32.32 fixed point
+  // (|error| <= rows * 2^-33 pixel, below the float32 weights' own rounding)
+  long long lfix = llrint(fma((double)m_lo, a.dl, l0) * 4294967296.0);
+  const long long dlfix = llrint(a.dl * 4294967296.0);
   T acc[VB];
 #pragma unroll
   for (int u = 0; u < VB; ++u) acc[u] = T(0);
@@ -427,19 +467,31 @@ __global__ __launch_bounds__(kBlock) void k_fwdg(const T* __restrict__ img, cons
     __syncthreads();
     if (m0 + kFgRows < m_hi) fetch(m0 + kFgRows);
     for (int r = 0; r < rows; ++r) {
-      const double l = fma((double)(m0 + r), a.dl, l0);
-      const double fl = floor(l);
-      const int idx = (int)fl - wlo_s[m0 - m_lo + r];
-      const T w1 = (T)(l - fl);
+      int idx;
+      T w1;
+      if constexpr (std::is_same<T, float>::value) {
+        idx = (int)(lfix >> 32) - wlo_s[m0 - m_lo + r];
+        w1 = (float)(unsigned)lfix * 2.3283064365386963e-10f;  // fraction * 2^-32
+        lfix += dlfix;
+      } else {
+        const double l = fma((double)(m0 + r), a.dl, l0);
+        const double fl = floor(l);
+        idx = (int)fl - wlo_s[m0 - m_lo + r];
+        w1 = (T)(l - fl);
+      }
       const T w0 = T(1) - w1;
+      // taps idx (weight w0) and idx+1 (w1): one is even, one odd
+      const bool odd = idx & 1;
+      const int se = (idx + 1) >> 1, so = kFgOdd + (idx >> 1);
+      const T we = odd ? w1 : w0, wo = odd ? w0 : w1;
 #pragma unroll
       for (int q = 0; q < NPL; ++q) {
-        const Pack<T, PV> s0 = win[q][r][idx];
-        const Pack<T, PV> s1 = win[q][r][idx + 1];
+        const Pack<T, PV> s0 = win[q][r][se];
+        const Pack<T, PV> s1 = win[q][r][so];
 #pragma unroll
         for (int e = 0; e < PV; ++e) {
-          acc[q * PV + e] = fma(w0, s0.v[e], acc[q * PV + e]);
-          acc[q * PV + e] = fma(w1, s1.v[e], acc[q * PV + e]);
+          acc[q * PV + e] = fma(we, s0.v[e], acc[q * PV + e]);
+          acc[q * PV + e] = fma(wo, s1.v[e], acc[q * PV + e]);
         }
       }
     }
@@ -519,6 +571,8 @@ template <typename T>
 struct BackArgs {
   const T* sino;            // interleaved [C][m][VB]
   const BackAngle* ang;     // [n_ang]
+  const BackAngleC* angc;   // [n_ang] compact records
+  double K;                 // angle-independent part of k_f
   int N, n_det, n_ang, V;
   // outputs
   T* out_t;                 // PLAIN: A^T s;  H: Hp;  INIT: p   (interleaved)
@@ -741,30 +795,39 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
   const int v0 = chunk * VB;
   const int nv = (MODE == BACK_WSQ) ? 1 : min(VB, A.V - v0);
   // geometry uses clamped coordinates so out-of-image threads stay inside the window;
-  // the angle constants are uniform -> scalar loads (shared table, scalar-cache resident)
-  const double djc = (double)min(j, N - 1), dic = (double)min(i, N - 1);
+  // the angle records are uniform -> scalar loads (shared table, scalar-cache resident)
+  const double c0 = 0.5 * (N - 1);
+  const double xi = (double)min(i, N - 1) - c0, yj = (double)min(j, N - 1) - c0;
   const int jhi = min(jb + kBTJ - 1, N - 1), ihi = min(ib + kBTI - 1, N - 1);
+  const double Kc = A.K;
 
   __shared__ Pack<T, PV> win[NPL][(MODE == BACK_WSQ) ? 1 : kBAngC][kBWin];
-  __shared__ int kmin_s[kBAngC];
+  __shared__ int4 kmin_s[kBAngC / 4];
   T acc[VB];
 #pragma unroll
   for (int u = 0; u < VB; ++u) acc[u] = T(0);
   const T* sino_c = A.sino + (size_t)chunk * m_rays * VB;
+  int t0c = 0;  // first angle of the current chunk (float64 weight path)
 
-  auto tap = [&](int t, int tt, T& w0, T& w1, Pack<T, PV> (&s0)[NPL], Pack<T, PV> (&s1)[NPL]) {
-    const BackAngle g = A.ang[t];
-    const double kf = fma(dic, g.Bi, fma(djc, g.Bj, g.B0));
+  auto tap = [&](const BackAngleC& g, int kmin, T& w0, T& w1, Pack<T, PV> (&s0)[NPL], Pack<T, PV> (&s1)[NPL],
+                 int tt) {
+    const double kf = fma(xi, g.Bi, fma(yj, g.Bj, Kc));
     const double kfl = floor(kf);
     const int k0 = (int)kfl;
     const T f = (T)(kf - kfl);
-    w0 = fmax(T(0), T(1) - f * (T)g.slope) * (T)g.L;
-    w1 = fmax(T(0), T(1) - (T(1) - f) * (T)g.slope) * (T)g.L;
+    if constexpr (std::is_same<T, float>::value) {
+      w0 = fmaxf(0.f, fmaf(-f, g.sLf, g.Lf));
+      w1 = fmaxf(0.f, fmaf(f, g.sLf, g.LmsLf));
+    } else {
+      const BackAngle& gd = A.ang[t0c + tt];
+      w0 = fmax(T(0), T(1) - f * (T)gd.slope) * (T)gd.L;
+      w1 = fmax(T(0), T(1) - (T(1) - f) * (T)gd.slope) * (T)gd.L;
+    }
     if constexpr (MODE == BACK_WSQ) {
       w0 = (k0 >= 0 && k0 <= n_det - 1) ? w0 : T(0);
       w1 = (k0 >= -1 && k0 <= n_det - 2) ? w1 : T(0);
     } else {
-      const int idx = k0 - kmin_s[tt];
+      const int idx = k0 - kmin;
 #pragma unroll
       for (int q = 0; q < NPL; ++q) {
         s0[q] = win[q][tt][idx];
@@ -792,18 +855,16 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
     if constexpr (MODE != BACK_WSQ) {
       __syncthreads();
       if ((int)threadIdx.x < nt) {
-        const BackAngle g = A.ang[t0 + threadIdx.x];
-        const double k00 = fma((double)ib, g.Bi, fma((double)jb, g.Bj, g.B0));
-        const double k01 = fma((double)ib, g.Bi, fma((double)jhi, g.Bj, g.B0));
-        const double k10 = fma((double)ihi, g.Bi, fma((double)jb, g.Bj, g.B0));
-        const double k11 = fma((double)ihi, g.Bi, fma((double)jhi, g.Bj, g.B0));
-        kmin_s[threadIdx.x] = (int)floor(fmin(fmin(k00, k01), fmin(k10, k11))) - 1;
+        const BackAngleC g = A.angc[t0 + threadIdx.x];
+        auto kf = [&](int ii, int jj) { return fma((double)ii - c0, g.Bi, fma((double)jj - c0, g.Bj, Kc)); };
+        const double kmn = fmin(fmin(kf(ib, jb), kf(ib, jhi)), fmin(kf(ihi, jb), kf(ihi, jhi)));
+        reinterpret_cast<int*>(kmin_s)[threadIdx.x] = (int)floor(kmn) - 1;
       }
       __syncthreads();
       for (int q = threadIdx.x; q < nt * kBWin * NPL; q += kBlock) {
         const int pl = q % NPL, aw = q / NPL;
         const int a = aw / kBWin, w = aw - a * kBWin;
-        const int k = kmin_s[a] + w;
+        const int k = reinterpret_cast<const int*>(kmin_s)[a] + w;
         Pack<T, PV> val;
         if (k >= 0 && k < n_det) {
           val = *reinterpret_cast<const Pack<T, PV>*>(sino_c + ((size_t)(t0 + a) * n_det + k) * VB + pl * PV);
@@ -815,19 +876,35 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
       }
       __syncthreads();
     }
+    // angles in groups of 4: the group's constants are scalar-loaded together (one
+    // lgkmcnt(0) per group -- scalar and LDS loads share that counter), then its taps
+    // run on LDS reads alone
+    t0c = t0;
     int tt = 0;
-    for (; tt + 1 < nt; tt += 2) {
-      T wa0, wa1, wb0, wb1;
-      Pack<T, PV> sa0[NPL], sa1[NPL], sb0[NPL], sb1[NPL];
-      tap(t0 + tt, tt, wa0, wa1, sa0, sa1);
-      tap(t0 + tt + 1, tt + 1, wb0, wb1, sb0, sb1);
-      fmac(wa0, wa1, sa0, sa1);
-      fmac(wb0, wb1, sb0, sb1);
+    for (; tt + 4 <= nt; tt += 4) {
+      BackAngleC g[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) g[u] = A.angc[t0 + tt + u];
+      int4 km = make_int4(0, 0, 0, 0);
+      if constexpr (MODE != BACK_WSQ) km = kmin_s[tt >> 2];
+      const int kms[4] = {km.x, km.y, km.z, km.w};
+#pragma unroll
+      for (int u = 0; u < 4; u += 2) {
+        T wa0, wa1, wb0, wb1;
+        Pack<T, PV> sa0[NPL], sa1[NPL], sb0[NPL], sb1[NPL];
+        tap(g[u], kms[u], wa0, wa1, sa0, sa1, tt + u);
+        tap(g[u + 1], kms[u + 1], wb0, wb1, sb0, sb1, tt + u + 1);
+        fmac(wa0, wa1, sa0, sa1);
+        fmac(wb0, wb1, sb0, sb1);
+      }
     }
-    if (tt < nt) {
+    for (; tt < nt; ++tt) {
+      const BackAngleC g = A.angc[t0 + tt];
+      int km = 0;
+      if constexpr (MODE != BACK_WSQ) km = reinterpret_cast<const int*>(kmin_s)[tt];
       T wa0, wa1;
       Pack<T, PV> sa0[NPL], sa1[NPL];
-      tap(t0 + tt, tt, wa0, wa1, sa0, sa1);
+      tap(g, km, wa0, wa1, sa0, sa1, tt);
       fmac(wa0, wa1, sa0, sa1);
     }
   }
