@@ -1115,6 +1115,61 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
   const double* xv = x + vo;
   const double* dv = din + 2 * vo;
   const double* ev = ein + 2 * vo;
+  if constexpr (!LAST) {
+    // Phase 1: shrink once per point of the tile plus one halo row (i0-1) and column (j0-1),
+    // keeping q = (d' - e') - (d - e) per component in LDS; tile points also store d', e'.
+    // Phase 2: K^T q at each tile pixel from LDS (the same four terms, in the same order,
+    // that the neighbour re-evaluation used), then r += mu K^T q, p = r.
+    constexpr int TI = EwMap<VB>::TI, HC = kTile + 1, HR = TI + 1;
+    // column-fastest: a wave reads runs of 33 consecutive pixels of one node
+    __shared__ double qx_s[HR][VB][HC], qy_s[HR][VB][HC];
+    for (int q = threadIdx.x; q < HR * HC * VB; q += kBlock) {
+      const int cc = q % HC, rest = q / HC;
+      const int u = rest % VB, rr = rest / VB;  // halo-shifted (row 0 = i0-1, col 0 = j0-1)
+      const int i = i0 + rr - 1, j = j0 + cc - 1;
+      const int vq = chunk * VB + u;
+      if (vq >= V || i < 0 || j < 0 || i >= N || j >= N) continue;
+      const size_t vqo = (size_t)vq * npix;
+      const double* xq = x + vqo;
+      const double* dq = din + 2 * vqo;
+      const double* eq = ein + 2 * vqo;
+      const int o = i * N + j;
+      double gx, gy, ndx, ndy;
+      grad_at(xq, N, i, j, gx, gy);
+      const double ux = gx + eq[o], uy = gy + eq[npix + o];
+      shrink2(ux, uy, tau, kind, ndx, ndy);
+      const double nex = ux - ndx, ney = uy - ndy;
+      qx_s[rr][u][cc] = (ndx - nex) - (dq[o] - eq[o]);
+      qy_s[rr][u][cc] = (ndy - ney) - (dq[npix + o] - eq[npix + o]);
+      if (rr >= 1 && cc >= 1) {
+        dout[2 * vqo + o] = ndx;
+        dout[2 * vqo + npix + o] = ndy;
+        eout[2 * vqo + o] = nex;
+        eout[2 * vqo + npix + o] = ney;
+      }
+    }
+    __syncthreads();
+    for (int rw = mp.isub; rw < TI; rw += EwMap<VB>::RPI) {
+      const int i = i0 + rw, j = j0 + mp.jj;
+      if (i >= N || j >= N) continue;
+      const int o = i * N + j;
+      T sv = T(0);
+      if (live) {
+        double kt = 0.0;
+        if (i <= N - 2) kt -= qx_s[rw + 1][mp.u][mp.jj + 1];
+        if (j <= N - 2) kt -= qy_s[rw + 1][mp.u][mp.jj + 1];
+        if (i >= 1) kt += qx_s[rw][mp.u][mp.jj + 1];
+        if (j >= 1) kt += qy_s[rw + 1][mp.u][mp.jj];
+        const double rn = r[vo + o] + mu * kt;
+        r[vo + o] = rn;
+        sv = (T)rn;
+      }
+      p[sbase + (size_t)o * VB + mp.u] = sv;
+      tl.t[rw][mp.jj][mp.u] = sv;
+    }
+    tile_store_T<T, VB>(tl, pT + sbase, N, i0, j0);
+    return;
+  }
   for (int rw = mp.isub; rw < EwMap<VB>::TI; rw += EwMap<VB>::RPI) {
     const int i = i0 + rw, j = j0 + mp.jj;
     if (i >= N || j >= N) continue;

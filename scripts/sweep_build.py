@@ -7,12 +7,16 @@ sys.path.insert(0, "distributed-inverse-problem-admm_amd")
 from admm_hip.build import build  # noqa: E402
 
 os.makedirs("variants", exist_ok=True)
-variants = [tuple(map(int, v.split("x"))) for v in sys.argv[1:]]  # ROWSxSEG
+# each argument: NAME:MACRO=VAL,MACRO=VAL   e.g.  ldsrec0:ADMM_BACK_LDSREC=0
+variants = []
+for a in sys.argv[1:]:
+    name, _, defs = a.partition(":")
+    variants.append((name, dict(kv.split("=") for kv in defs.split(",") if kv)))
 
 
 def one(v):
-    r, s = v
-    return build(force=True, out=f"variants/lib_r{r}_s{s}.so", defines={"ADMM_FG_ROWS": r, "ADMM_FG_SEG": s})
+    name, defs = v
+    return build(force=True, out=f"variants/lib_{name}.so", defines=defs)
 
 
 with ThreadPoolExecutor(4) as ex:
