@@ -190,6 +190,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
   double* c = (double*)C->c.p;
   double* redH = (double*)C->redH.p;
   const dim3 tg = tile_grid(C, nch, VB);
+  const dim3 cgg((N + kTile - 1) / kTile, (N + kCgRows - 1) / kCgRows, nch);
   const int Pb = C->P_back;
 
   // 1. neighbour gather: c = sum_j q_ij (z_ij - y_ij,i); xs = (T) x (+ transpose)
@@ -239,7 +240,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
       a.mu = B.mu;
       RET((launch_back<T, VB, BACK_H>(C, a, V, s)));
       RET(launch_reduce((double*)C->partH.p, 5 * V, Pb, redH, 1, 1, 0, s));
-      hipLaunchKernelGGL((k_cg_update<T, VB>), tg, dim3(kBlock), 0, s, B.x_ext, r, p, pT, Hp, redH, N, V);
+      hipLaunchKernelGGL((k_cg_update<T, VB>), cgg, dim3(kBlock), 0, s, B.x_ext, r, p, pT, Hp, redH, N, V);
       CHECK_LAUNCH();
     }
     const bool last = (t + 1 == Tt);

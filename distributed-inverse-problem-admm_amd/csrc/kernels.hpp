@@ -1028,46 +1028,67 @@ __global__ __launch_bounds__(kBlock) void k_transpose(const T* __restrict__ in, 
 // CG step from the five reductions of the preceding BACK_H launch (oracle/node_solver.py):
 //   alpha = r.p / p.Hp (exact line search),  rr' = rr - 2 alpha rHp + alpha^2 HpHp,  beta = rr'/rr
 //   x += alpha p;  r -= alpha Hp;  p = r + beta p  (p also written transposed)
+// One thread per pixel, all VB nodes of the chunk: the interleaved p / Hp samples are
+// one 32-B vector per lane and every node's float64 x / r is read in 32-pixel (256-B)
+// runs (a node-per-lane mapping splits those into 64-B pieces across 8 arrays 2 MB apart).
+constexpr int kCgRows = kBlock / kTile;  // 8 rows x 32 columns per block
+
 template <typename T, int VB>
 __global__ __launch_bounds__(kBlock) void k_cg_update(double* __restrict__ x, double* __restrict__ r,
                                                       T* __restrict__ p, T* __restrict__ pT,
                                                       const T* __restrict__ Hp, const double* __restrict__ redH,
                                                       int N, int V) {
-  __shared__ TileT<T, VB> tl;
-  const EwMap<VB> mp;
-  const int chunk = blockIdx.z, v = chunk * VB + mp.u;
-  const bool live = v < V;
+  __shared__ T tl[kCgRows][kTile + 1][VB];
+  __shared__ double ab_s[VB][2];
+  const int chunk = blockIdx.z, v0 = chunk * VB;
   const int npix = N * N;
   const size_t sbase = (size_t)chunk * npix * VB;
-  double alpha = 0.0, beta = 0.0;
-  if (live) {
-    const double* S = redH + 5 * v;
-    const double pHp = S[0], rHp = S[1], HH = S[2], rr = S[3], rp = S[4];
-    alpha = (pHp != 0.0) ? rp / pHp : 0.0;
-    double rrn = rr - 2.0 * alpha * rHp + alpha * alpha * HH;
-    rrn = fmax(rrn, 0.0);
-    beta = (rr != 0.0) ? rrn / rr : 0.0;
-  }
-  const int i0 = blockIdx.y * EwMap<VB>::TI, j0 = blockIdx.x * kTile;
-  for (int rw = mp.isub; rw < EwMap<VB>::TI; rw += EwMap<VB>::RPI) {
-    const int i = i0 + rw, j = j0 + mp.jj;
-    if (i < N && j < N) {
-      const int pix = i * N + j;
-      const size_t so = sbase + (size_t)pix * VB + mp.u;
-      T np = T(0);
-      if (live) {
-        const size_t o = (size_t)v * npix + pix;
-        const double pd = (double)p[so];
-        x[o] += alpha * pd;
-        const double rn = r[o] - alpha * (double)Hp[so];
-        r[o] = rn;
-        np = (T)(rn + beta * pd);
-      }
-      p[so] = np;
-      tl.t[rw][mp.jj][mp.u] = np;
+  if ((int)threadIdx.x < VB) {
+    const int v = v0 + threadIdx.x;
+    double alpha = 0.0, beta = 0.0;
+    if (v < V) {
+      const double* S = redH + 5 * v;
+      const double pHp = S[0], rHp = S[1], HH = S[2], rr = S[3], rp = S[4];
+      alpha = (pHp != 0.0) ? rp / pHp : 0.0;
+      double rrn = rr - 2.0 * alpha * rHp + alpha * alpha * HH;
+      rrn = fmax(rrn, 0.0);
+      beta = (rr != 0.0) ? rrn / rr : 0.0;
     }
+    ab_s[threadIdx.x][0] = alpha;
+    ab_s[threadIdx.x][1] = beta;
   }
-  tile_store_T<T, VB>(tl, pT + sbase, N, i0, j0);
+  __syncthreads();
+  const int jj = threadIdx.x % kTile, ii = threadIdx.x / kTile;
+  const int i0 = blockIdx.y * kCgRows, j0 = blockIdx.x * kTile;
+  const int i = i0 + ii, j = j0 + jj;
+  if (i < N && j < N) {
+    const int pix = i * N + j;
+    T pv[VB], hv[VB], np[VB];
+    gload<T, VB>(p + sbase + (size_t)pix * VB, pv);
+    gload<T, VB>(Hp + sbase + (size_t)pix * VB, hv);
+#pragma unroll
+    for (int u = 0; u < VB; ++u) {
+      np[u] = T(0);
+      if (v0 + u < V) {
+        const size_t o = (size_t)(v0 + u) * npix + pix;
+        const double alpha = ab_s[u][0], beta = ab_s[u][1];
+        const double pd = (double)pv[u];
+        x[o] += alpha * pd;
+        const double rn = r[o] - alpha * (double)hv[u];
+        r[o] = rn;
+        np[u] = (T)(rn + beta * pd);
+      }
+      tl[ii][jj][u] = np[u];
+    }
+    gstore<T, VB>(p + sbase + (size_t)pix * VB, np);
+  }
+  __syncthreads();
+  // transposed copy: pT[j][i][u], runs of kCgRows x VB samples per column
+  const int u = threadIdx.x % VB, rr_ = (threadIdx.x / VB) % kCgRows, c0 = threadIdx.x / (VB * kCgRows);
+  for (int c = c0; c < kTile; c += kBlock / (VB * kCgRows)) {
+    const int jc = j0 + c, ic = i0 + rr_;
+    if (jc < N && ic < N) pT[sbase + ((size_t)jc * N + ic) * VB + u] = tl[rr_][c][u];
+  }
 }
 
 // split-Bregman (d, e) update after a CG solve:
