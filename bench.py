@@ -84,7 +84,7 @@ def cpu_baseline(seconds_budget=20.0):
 # (scripts/pmc.sh + scripts/traffic_summary.py; 2 x FETCH_SIZE + WRITE_SIZE per the
 # MI355X_MICROARCH.md gfx950 correction).  PMC counters cannot be read inside this run.
 TRAFFIC_FILE = "profiles/r1_traffic.json"
-FWD_KERNELS = ("admm::k_fwdg<float, 8>", "admm::k_fwd_combine<float, 8, 0>")
+FWD_KERNELS = ("admm::k_fwdg<float, 8>",)
 
 
 def pmc_traffic(names):
@@ -192,7 +192,8 @@ def main():
             "graph": "ring", "parallelism": f"graph-node shards x{world}",
         },
         "roofline": {
-            "kernel": "k_fwdg<float,8> + k_fwd_combine<float,8,0> (Joseph forward projector, angle-grouped)",
+            "kernel": "k_fwdg<float,8> (Joseph forward projector taps, angle-grouped; its 8-segment "
+                      "partial sums are added by k_fwd_combine, ~5 us, not included)",
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,

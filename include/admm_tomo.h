@@ -172,8 +172,9 @@ int admm_node_update(admm_ctx* ctx, void* stream);
  * slot of the batch is processed; x_ext halo rows must be current. */
 int admm_consensus(admm_ctx* ctx, void* stream);
 /* Average duration (ms) of `reps` back-to-back launches of the forward
- * projector on the bound batch's current x, timed with HIP events on `stream`.
- * Measurement helper for bench.py; synchronises. */
+ * projector's tap kernel (k_fwdg, which makes every sample tap; its segment
+ * partial sums are not combined) on the bound batch's current x, timed with HIP
+ * events on `stream`.  Measurement helper for bench.py; synchronises. */
 int admm_time_forward(admm_ctx* ctx, int reps, void* stream, double* ms_out);
 
 /* --- per-pixel edge masks for masked precisions (setup) --- */
