@@ -29,6 +29,9 @@ class HaloExchange:
         if not self.active:
             return
         dev = x_ext.device
+        # gloo moves host tensors only: device images are staged through host copies
+        # (tests and 1-GPU rehearsals; RCCL reads and writes HBM directly)
+        self.stage = x_ext.is_cuda and dist.get_backend(group) == "gloo"
         self.mode = "allgather" if plan.use_allgather() else "p2p"
         V = plan.V
         if self.mode == "allgather":
@@ -63,19 +66,41 @@ class HaloExchange:
         p = self.plan
         if self.mode == "allgather":
             self.sendbuf[: self.V].copy_(self.x[: self.V])
-            dist.all_gather_into_tensor(self.full, self.sendbuf, group=self.group)
+            if self.stage:
+                full = self.full.cpu()
+                dist.all_gather_into_tensor(full, self.sendbuf.cpu(), group=self.group)
+                self.full.copy_(full)
+            else:
+                dist.all_gather_into_tensor(self.full, self.sendbuf, group=self.group)
             if len(p.halo_nodes):
                 self.x[self.V:].copy_(self.full.index_select(0, self.halo_idx))
             return
-        ops = []
+        ops, landing = [], []
         for peer, rows, buf in self.sends:
             torch.index_select(self.x, 0, rows, out=buf)
-            ops.append(dist.P2POp(dist.isend, buf, peer, group=self.group))
+            ops.append(dist.P2POp(dist.isend, buf.cpu() if self.stage else buf, peer, group=self.group))
         for peer, r0, cnt in self.recvs:
-            ops.append(dist.P2POp(dist.irecv, self.x[r0:r0 + cnt], peer, group=self.group))
+            dst = self.x[r0:r0 + cnt]
+            if self.stage:
+                host = torch.empty(dst.shape, dtype=dst.dtype)
+                landing.append((dst, host))
+                dst = host
+            ops.append(dist.P2POp(dist.irecv, dst, peer, group=self.group))
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
+        for dst, host in landing:
+            dst.copy_(host)
+
+
+def _all_reduce_sum(t: torch.Tensor, group=None) -> torch.Tensor:
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        host = t.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+        t.copy_(host)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t
 
 
 def assemble_stats(plan: ShardPlan, node_stats: torch.Tensor, edge_stats: torch.Tensor, group=None):
@@ -99,7 +124,7 @@ def assemble_stats(plan: ShardPlan, node_stats: torch.Tensor, edge_stats: torch.
         gids = torch.tensor([plan.stored_edges[k] for k in owned], dtype=torch.long, device=dev)
         ev = buf[plan.V_total * ns:].view(E, es)
         ev.index_copy_(0, gids, edge_stats.index_select(0, slots))
-    dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+    _all_reduce_sum(buf, group)
     host = buf.to("cpu")
     return host[: plan.V_total * ns].view(plan.V_total, ns), host[plan.V_total * ns:].view(E, es)
 
@@ -112,5 +137,4 @@ def gather_images(plan: ShardPlan, x_local: torch.Tensor, group=None) -> torch.T
     buf = torch.zeros((plan.V_total, n), dtype=x_local.dtype, device=x_local.device)
     lo = plan.local_nodes[0] if plan.local_nodes else 0
     buf[lo:lo + plan.V].copy_(x_local)
-    dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
-    return buf
+    return _all_reduce_sum(buf, group)
