@@ -367,8 +367,16 @@ __global__ __launch_bounds__(kFwdBlock) void k_fwd(const T* __restrict__ img, co
 #ifndef ADMM_FG_SEG
 #define ADMM_FG_SEG 8
 #endif
+#ifndef ADMM_FG_G
+#define ADMM_FG_G 16
+#endif
+#ifndef ADMM_FG_WIN
+#define ADMM_FG_WIN 256
+#endif
 constexpr int kFgRows = ADMM_FG_ROWS;  // rows staged per LDS chunk
-constexpr int kFgWin = 160;
+constexpr int kFgG = ADMM_FG_G;        // max angles (waves) per block
+constexpr int kFgThreads = 64 * kFgG;
+constexpr int kFgWin = ADMM_FG_WIN;    // staged window width (pixels)
 constexpr int kFgSeg = ADMM_FG_SEG;    // row segments (partial sums) per ray
 constexpr int kFgHalf = kFgWin / 2;        // slots per parity
 constexpr int kFgOdd = kFgHalf + 4;        // odd half-window offset (+64 B bank shift)
@@ -386,12 +394,12 @@ struct FgGroup {
 };
 
 template <typename T, int VB>
-__global__ __launch_bounds__(kBlock) void k_fwdg(const T* __restrict__ img, const T* __restrict__ imgT,
+__global__ __launch_bounds__(kFgThreads) void k_fwdg(const T* __restrict__ img, const T* __restrict__ imgT,
                                                  T* __restrict__ part, const FwdAngle* __restrict__ ang,
                                                  const FgGroup* __restrict__ groups, int N, int n_det, int n_ang,
                                                  int V) {
   constexpr int NPL = Planes<T, VB>::NPL, PV = Planes<T, VB>::PV;
-  constexpr int PER = (kFgRows * kFgWin * NPL + kBlock - 1) / kBlock;  // staged packs per thread
+  constexpr int PER = (kFgRows * kFgWin * NPL + kFgThreads - 1) / kFgThreads;  // staged packs per thread
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int kc = blockIdx.x;
   const FgGroup gr = groups[blockIdx.y];
@@ -408,16 +416,21 @@ __global__ __launch_bounds__(kBlock) void k_fwdg(const T* __restrict__ img, cons
   const int nrows = m_hi - m_lo;
 
   __shared__ Pack<T, PV> win[NPL][kFgRows][kFgRow];
-  __shared__ int wlo_s[(4096 + kFgSeg - 1) / kFgSeg];  // every row window of the segment (N <= 4096)
-  for (int r = threadIdx.x; r < nrows; r += kBlock) {
+  // every row window of the segment (N <= 4096): origin and the width actually touched
+  __shared__ int wlo_s[(4096 + kFgSeg - 1) / kFgSeg];
+  __shared__ int wnum_s[(4096 + kFgSeg - 1) / kFgSeg];
+  for (int r = threadIdx.x; r < nrows; r += kFgThreads) {
     const double dm = (double)(m_lo + r);
-    double lmin = 1e300;
+    double lmin = 1e300, lmax = -1e300;
     for (int gg = 0; gg < gr.G; ++gg) {
       const FwdAngle b = ang[gr.t0 + gg];
-      lmin = fmin(lmin, fma(dm, b.dl, fma((double)klo, b.A1, b.A0)));
-      lmin = fmin(lmin, fma(dm, b.dl, fma((double)khi, b.A1, b.A0)));
+      const double la = fma(dm, b.dl, fma((double)klo, b.A1, b.A0));
+      const double lb = fma(dm, b.dl, fma((double)khi, b.A1, b.A0));
+      lmin = fmin(lmin, fmin(la, lb));
+      lmax = fmax(lmax, fmax(la, lb));
     }
     wlo_s[r] = (int)floor(lmin) - 1;
+    wnum_s[r] = min(kFgWin, (int)floor(lmax) - (int)floor(lmin) + 3);
   }
   __syncthreads();
 
@@ -428,10 +441,11 @@ __global__ __launch_bounds__(kBlock) void k_fwdg(const T* __restrict__ img, cons
     const int rows = min(kFgRows, m_hi - m0);
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
-      const int q = threadIdx.x + e * kBlock;
+      const int q = threadIdx.x + e * kFgThreads;
       const int pl = q % NPL, rw = q / NPL;
       const int r = rw / kFgWin, w = rw - r * kFgWin;
-      const int col = (r < rows) ? wlo_s[m0 - m_lo + r] + w : -1;
+      // only the row's touched width is fetched (the rest of the window is never read)
+      const int col = (r < rows && w < wnum_s[m0 - m_lo + r]) ? wlo_s[m0 - m_lo + r] + w : -1;
       if (q < kFgRows * kFgWin * NPL && col >= 0 && col < N) {
         stage[e] = *reinterpret_cast<const Pack<T, PV>*>(src + ((size_t)(m0 + r) * N + col) * VB + pl * PV);
       } else {
@@ -443,7 +457,7 @@ __global__ __launch_bounds__(kBlock) void k_fwdg(const T* __restrict__ img, cons
   auto commit = [&]() {
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
-      const int q = threadIdx.x + e * kBlock;
+      const int q = threadIdx.x + e * kFgThreads;
       if (q < kFgRows * kFgWin * NPL) {
         const int pl = q % NPL, rw = q / NPL;
         const int r = rw / kFgWin, w = rw - r * kFgWin;
@@ -459,13 +473,16 @@ __global__ __launch_bounds__(kBlock) void k_fwdg(const T* __restrict__ img, cons
   T acc[VB];
 #pragma unroll
   for (int u = 0; u < VB; ++u) acc[u] = T(0);
-  fetch(m_lo);
+#ifndef ADMM_FG_EXPT
+#define ADMM_FG_EXPT 0  // timing diagnostics only: 1 = no tap loop, 2 = no staging
+#endif
+  if (ADMM_FG_EXPT != 2) fetch(m_lo);
   for (int m0 = m_lo; m0 < m_hi; m0 += kFgRows) {
-    const int rows = min(kFgRows, m_hi - m0);
+    const int rows = (ADMM_FG_EXPT == 1) ? 0 : min(kFgRows, m_hi - m0);
     __syncthreads();  // previous chunk's readers are done
-    commit();
+    if (ADMM_FG_EXPT != 2) commit();
     __syncthreads();
-    if (m0 + kFgRows < m_hi) fetch(m0 + kFgRows);
+    if (ADMM_FG_EXPT != 2 && m0 + kFgRows < m_hi) fetch(m0 + kFgRows);
     for (int r = 0; r < rows; ++r) {
       int idx;
       T w1;
