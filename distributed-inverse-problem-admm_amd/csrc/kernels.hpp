@@ -792,9 +792,15 @@ __device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j
 // Two angles are processed per iteration to keep 4 LDS reads in flight.
 constexpr int kBTJ = 64;
 constexpr int kBTI = 4;
-constexpr int kBAngC = 16;
+#ifndef ADMM_BK_ANGC
+#define ADMM_BK_ANGC 16
+#endif
+constexpr int kBAngC = ADMM_BK_ANGC;  // angles per staged sinogram-window chunk
 constexpr int kBWin = 72;
 
+#ifndef ADMM_BK_EXPT
+#define ADMM_BK_EXPT 0  // timing diagnostics only: 1 = no angle loop, 2 = no window loads, 3 = no H epilogue
+#endif
 template <typename T, int VB, int MODE>
 __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
   constexpr int NQ = (MODE == BACK_H) ? 5 : (MODE == BACK_DIAG) ? 4 : 1;
@@ -883,7 +889,7 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
         const int a = aw / kBWin, w = aw - a * kBWin;
         const int k = reinterpret_cast<const int*>(kmin_s)[a] + w;
         Pack<T, PV> val;
-        if (k >= 0 && k < n_det) {
+        if (ADMM_BK_EXPT != 2 && k >= 0 && k < n_det) {
           val = *reinterpret_cast<const Pack<T, PV>*>(sino_c + ((size_t)(t0 + a) * n_det + k) * VB + pl * PV);
         } else {
 #pragma unroll
@@ -897,7 +903,7 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
     // lgkmcnt(0) per group -- scalar and LDS loads share that counter), then its taps
     // run on LDS reads alone
     t0c = t0;
-    int tt = 0;
+    int tt = (ADMM_BK_EXPT == 1) ? nt : 0;
     for (; tt + 4 <= nt; tt += 4) {
       BackAngleC g[4];
 #pragma unroll
@@ -931,7 +937,13 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
   for (int u = 0; u < VB; ++u)
 #pragma unroll
     for (int q = 0; q < NQ; ++q) pq[u][q] = 0.0;
-  if (inb) back_epilogue<T, VB, MODE, NQ>(A, i, j, chunk, v0, nv, acc, pq);
+  if (inb) {
+    if constexpr (ADMM_BK_EXPT == 3 && MODE == BACK_H) {
+      gstore<T, VB>(A.out_t + (size_t)chunk * N * N * VB + (size_t)(i * N + j) * VB, acc);
+    } else {
+      back_epilogue<T, VB, MODE, NQ>(A, i, j, chunk, v0, nv, acc, pq);
+    }
+  }
 
   if constexpr (MODE == BACK_H || MODE == BACK_DIAG) {
     constexpr int NV = ((VB * NQ + 15) / 16) * 16;
