@@ -10,6 +10,8 @@ residual/statistics readback the reference's stop test needs.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
+    python bench.py --config C2|C3|C4|C5     (BASELINE.json configs[1..4], fixed node count,
+                                               sharded over however many ranks run it)
 
 Rank 0 prints one JSON line.  The forward projector's average launch time is
 measured live with HIP events on the stream it runs on; its algorithmic
@@ -38,14 +40,44 @@ TV_ITERS, CG_ITERS = 10, 5
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
-def node_bytes(N, a, tv, cg):
-    """Algorithmic sample-touch bytes of one x-update (float32)."""
+# BASELINE.json configs[1..4]: image side, total graph nodes, graph, dtype, TV
+CONFIGS = {
+    "C2": dict(N=256, nodes=8, graph="ring", dtype="float32", tv="iso"),
+    "C3": dict(N=512, nodes=16, graph="ring", dtype="float32", tv="iso"),
+    "C4": dict(N=1024, nodes=32, graph="er", dtype="float32", tv="iso"),
+    "C5": dict(N=2048, nodes=64, graph="complete", dtype="float64", tv="aniso"),
+    # C5's per-GPU share (8 of its 64 nodes at 8 GPUs) on one GPU: a 1-GPU rehearsal of the
+    # 2048^2 float64 anisotropic x-update (complete graph of the 8 local nodes)
+    "C5s": dict(N=2048, nodes=8, graph="complete", dtype="float64", tv="aniso"),
+}
+
+
+def make_graph(kind, V):
+    import math
+    import networkx as nx
+    if kind == "ring":
+        return nx.cycle_graph(V)
+    if kind == "complete":
+        return nx.complete_graph(V)
+    # Erdos-Renyi p = 2 ln V / V, seed 0, resampled (seed + 1) until connected
+    p = 2.0 * math.log(V) / V
+    seed = 0
+    while True:
+        G = nx.erdos_renyi_graph(V, p, seed=seed)
+        if nx.is_connected(G):
+            return G
+        seed += 1
+
+
+def node_bytes(N, a, tv, cg, sample_bytes=4):
+    """Algorithmic sample-touch bytes of one x-update (4-byte samples, 8 in C5)."""
     m = a * N
     n = N * N
-    B_A = 4 * m * (2 * N + 1)
-    B_At = 4 * n * (2 * a + 1)
-    B_cg = B_A + B_At + 24 * n + 56 * n
-    return B_A, B_At, tv * (cg * B_cg + 108 * n) + B_At + 4 * n * (3 * 2 + 2)
+    sb = sample_bytes
+    B_A = sb * m * (2 * N + 1)
+    B_At = sb * n * (2 * a + 1)
+    B_cg = B_A + B_At + 6 * sb * n + 14 * sb * n
+    return B_A, B_At, tv * (cg * B_cg + 27 * sb * n) + B_At + sb * n * (3 * 2 + 2)
 
 
 def cpu_baseline(seconds_budget=20.0):
@@ -103,6 +135,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fwd-reps", type=int, default=20)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
+                    help="run a BASELINE.json config (fixed node count) instead of the default workload")
     args = ap.parse_args()
 
     import networkx as nx
@@ -131,17 +165,24 @@ def main():
     from admm_hip.plan import make_plan
     from admm_hip.solver import NodeBatch, make_operators
 
-    V_total = NODES_PER_GPU * world
-    ops = make_operators(N_IMG, V_total, angles_total=ANGLES_PER_NODE * V_total, device=local_rank)
+    if args.config:
+        cfg = CONFIGS[args.config]
+        n_img, V_total, dtype, tv_kind = cfg["N"], cfg["nodes"], cfg["dtype"], cfg["tv"]
+        G = make_graph(cfg["graph"], V_total)
+        angles_total = max(180, 3 * n_img)  # block_2_load_odl_data.py:31-38
+    else:
+        n_img, V_total, dtype, tv_kind = N_IMG, NODES_PER_GPU * world, "float32", "iso"
+        G = nx.cycle_graph(V_total)
+        angles_total = ANGLES_PER_NODE * V_total
+    ops = make_operators(n_img, V_total, angles_total=angles_total, dtype=dtype, device=local_rank)
     geom = ops[0].geom
-    G = nx.cycle_graph(V_total)
     plan = make_plan(G, V_total, world, rank)
-    ph = shepp_logan(N_IMG)
+    ph = shepp_logan(n_img)
     lo = plan.local_nodes[0]
     sinos = dict(zip(plan.local_nodes,
                      make_sinograms([ops[g] for g in plan.local_nodes], ph, 0.005, seed=1000 + lo)))
     Wi, Q = make_precisions(ops)  # one W kernel launch: every node shares the geometry
-    nb = NodeBatch(geom, "float32", plan, sinos, Q, RHO, LAM, 10 * LAM, TV_ITERS, CG_ITERS, "iso",
+    nb = NodeBatch(geom, dtype, plan, sinos, Q, RHO, LAM, 10 * LAM, TV_ITERS, CG_ITERS, tv_kind,
                    ph, local_rank)
     halo = HaloExchange(plan, nb.x_ext)
     if world > 1:
@@ -175,9 +216,19 @@ def main():
 
     # live measurement of the dominant kernel (forward projector) on its stream
     fwd_ms = nb.time_forward(args.fwd_reps)
-    B_A, B_At, B_node = node_bytes(N_IMG, ANGLES_PER_NODE, TV_ITERS, CG_ITERS)
+    a_node = geom.n_angles
+    sbytes = 8 if dtype == "float64" else 4
+    B_A, B_At, B_node = node_bytes(n_img, a_node, TV_ITERS, CG_ITERS, sbytes)
     achieved = B_A * plan.V / (fwd_ms * 1e-3) / 1e9
-    fwd_traffic = pmc_traffic(FWD_KERNELS)
+    fwd_traffic = pmc_traffic(FWD_KERNELS) if not args.config else None
+    if args.config:
+        workload = (f"{args.config}: {n_img}^2, {V_total} graph nodes ({CONFIGS[args.config]['graph']}), "
+                    f"{a_node} angles/node, {dtype} samples, {tv_kind} TV, lam=0.02 rho=2, split-Bregman "
+                    f"{TV_ITERS}x{CG_ITERS} CG, one step = one outer ADMM iteration")
+    else:
+        workload = (f"512^2, {NODES_PER_GPU} graph nodes/GPU x {ANGLES_PER_NODE} angles (ring of "
+                    f"{V_total}; N=2 == BASELINE configs[2]), lam=0.02 rho=2, split-Bregman "
+                    f"{TV_ITERS}x{CG_ITERS} CG, one step = one outer ADMM iteration")
     result = {
         "metric": "ADMM node-updates/sec (whole node), 512² phantom; rel-Fro vs CPU ref",
         "value": value,
@@ -187,20 +238,20 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": 1e3 * el / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.config else "weak",
         "vs_baseline": None,
-        "dtype": "f32 samples / f64 state",
+        "dtype": ("f64 samples / f64 state" if dtype == "float64" else "f32 samples / f64 state"),
         "data": "synthetic modified Shepp-Logan, on-GPU Gaussian noise sigma=0.005",
         "config": {
-            "workload": f"512^2, {NODES_PER_GPU} graph nodes/GPU x {ANGLES_PER_NODE} angles (ring of "
-                        f"{V_total}; N=2 == BASELINE configs[2]), lam=0.02 rho=2, split-Bregman "
-                        f"{TV_ITERS}x{CG_ITERS} CG, one step = one outer ADMM iteration",
-            "image": N_IMG, "nodes": V_total, "angles_per_node": ANGLES_PER_NODE,
-            "graph": "ring", "parallelism": f"graph-node shards x{world}",
+            "workload": workload,
+            "image": n_img, "nodes": V_total, "angles_per_node": a_node,
+            "graph": CONFIGS[args.config]["graph"] if args.config else "ring",
+            "parallelism": f"graph-node shards x{world}",
         },
         "roofline": {
-            "kernel": "k_fwdg<float,8> (Joseph forward projector taps, angle-grouped; its 8-segment "
-                      "partial sums are added by k_fwd_combine, ~5 us, not included)",
+            "kernel": f"k_fwdg<{'double' if dtype == 'float64' else 'float'},{nb.ctx_vb}> (Joseph forward "
+                      "projector taps, angle-grouped; its 8-segment partial sums are added by "
+                      "k_fwd_combine, ~5 us at 512^2, not included)",
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
@@ -216,7 +267,7 @@ def main():
         "node_update_bytes": B_node,
         "node_update_gbs": B_node * value / world / 1e9,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.config:
         result["cpu_baseline"] = cpu_baseline()
         result["cpu_baseline"]["cores"] = 1
     if rank == 0:

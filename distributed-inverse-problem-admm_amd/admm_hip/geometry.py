@@ -77,6 +77,9 @@ class _Ctx:
 
     def __init__(self, geom: ParallelBeamGeometry, dtype: str, device: int, max_images: int = 64):
         self.lib = _lib.load()
+        # the library keeps 32-bit element offsets per batch: cap the image count so
+        # max_images x max(n, m) x 8 bytes stays below 2^31 (apply() splits larger batches)
+        max_images = max(1, min(max_images, ((1 << 31) - 1) // (8 * max(geom.n, geom.m))))
         self.geom = geom
         self.dtype = dtype
         self.device = device

@@ -144,6 +144,12 @@ class NodeBatch:
         return self.plan.V
 
     @property
+    def ctx_vb(self) -> int:
+        """Node-interleave width the library uses for this batch (admm_tomo.hip vb_for)."""
+        V = self.plan.V
+        return 8 if V >= 5 else 4 if V >= 3 else V
+
+    @property
     def x_local(self) -> torch.Tensor:
         return self.x_ext[: self.plan.V]
 
