@@ -48,7 +48,7 @@ CONFIGS = {
     "C5": dict(N=2048, nodes=64, graph="complete", dtype="float64", tv="aniso"),
     # C5's per-GPU share (8 of its 64 nodes at 8 GPUs) on one GPU: a 1-GPU rehearsal of the
     # 2048^2 float64 anisotropic x-update (complete graph of the 8 local nodes)
-    "C5s": dict(N=2048, nodes=8, graph="complete", dtype="float64", tv="aniso"),
+    "C5s": dict(N=2048, nodes=8, graph="complete", dtype="float64", tv="aniso", angles_per_node=96),
 }
 
 
@@ -170,6 +170,8 @@ def main():
         n_img, V_total, dtype, tv_kind = cfg["N"], cfg["nodes"], cfg["dtype"], cfg["tv"]
         G = make_graph(cfg["graph"], V_total)
         angles_total = max(180, 3 * n_img)  # block_2_load_odl_data.py:31-38
+        if "angles_per_node" in cfg:  # a share of a larger config keeps its per-node angle count
+            angles_total = cfg["angles_per_node"] * V_total
     else:
         n_img, V_total, dtype, tv_kind = N_IMG, NODES_PER_GPU * world, "float32", "iso"
         G = nx.cycle_graph(V_total)
