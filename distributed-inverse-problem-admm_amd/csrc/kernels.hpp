@@ -483,7 +483,9 @@ __global__ __launch_bounds__(kFgThreads) void k_fwdg(const T* __restrict__ img, 
     if (ADMM_FG_EXPT != 2) commit();
     __syncthreads();
     if (ADMM_FG_EXPT != 2 && m0 + kFgRows < m_hi) fetch(m0 + kFgRows);
-    for (int r = 0; r < rows; ++r) {
+#pragma unroll
+    for (int r = 0; r < kFgRows; ++r) {  // unrolled: the chunk's LDS reads can all be in flight
+      if (r >= rows) break;
       int idx;
       T w1;
       if constexpr (std::is_same<T, float>::value) {
