@@ -159,7 +159,7 @@ int launch_back(admm_ctx* C, BackArgs<T> a, int V, hipStream_t s) {
   a.V = V;
   const int N = C->g.N;
   dim3 grid((N + kBTJ - 1) / kBTJ, (N + kBTI - 1) / kBTI, MODE == BACK_WSQ ? 1 : (V + VB - 1) / VB);
-  hipLaunchKernelGGL((k_back<T, VB, MODE>), grid, dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL((k_back<T, VB, MODE>), grid, dim3(kBkThreads), 0, s, a);
   CHECK_LAUNCH();
   return ADMM_OK;
 }

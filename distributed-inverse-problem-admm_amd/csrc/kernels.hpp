@@ -147,12 +147,13 @@ __device__ __forceinline__ void block_reduce(double (&v)[NQ], double* lds /* >= 
 // keeps half of its values and adds its partner's copy of that half (NV/2 + NV/4
 // + NV/8 + NV/16 shuffles instead of 6*NV), then a plain butterfly over offsets
 // 2, 1 on the last NV/16.  Lanes with (lane & 3) == 0 then hold the wave totals;
-// the 4 waves are combined in LDS in fixed order.  On return thread t < NV of the
+// the NW waves are combined in LDS in a fixed pairwise tree.  On return thread t < NV of the
 // block can read total t from out_lds[t].  Fixed order -> bitwise reproducible.
 // ---------------------------------------------------------------------------
-template <int NV>
-__device__ __forceinline__ void block_reduce_rs(double (&v)[NV], double* lds /* >= 4*NV */,
+template <int NV, int NW = 4>
+__device__ __forceinline__ void block_reduce_rs(double (&v)[NV], double* lds /* >= NW*NV */,
                                                 double* out_lds /* >= NV */) {
+  static_assert(NW == 4 || NW == 8 || NW == 16, "NW = 4, 8 or 16 waves");
   static_assert(NV % 16 == 0, "NV must be a multiple of 16");
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -200,7 +201,15 @@ __device__ __forceinline__ void block_reduce_rs(double (&v)[NV], double* lds /* 
   __syncthreads();
   if ((int)threadIdx.x < NV) {
     const int t = threadIdx.x;
-    out_lds[t] = (lds[t] + lds[NV + t]) + (lds[2 * NV + t] + lds[3 * NV + t]);
+    // fixed pairwise tree over the NW wave totals
+    double w[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) w[q] = lds[q * NV + t];
+#pragma unroll
+    for (int h = NW / 2; h >= 1; h >>= 1)
+#pragma unroll
+      for (int q = 0; q < h; ++q) w[q] = w[2 * q] + w[2 * q + 1];
+    out_lds[t] = w[0];
   }
   __syncthreads();
 }
@@ -784,7 +793,7 @@ __device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j
   }
 }
 
-// Back projector.  Block = 64 (j) x 4 (i) pixel tile, one pixel per thread.
+// Back projector.  Block = 64 (j) x kBTI (i) pixel tile, one pixel per thread.
 // Per chunk of kBAngC angles the block stages, for each angle, the window of
 // kBWin detector bins its tile can touch (from the floor of the smallest corner
 // k_f, minus 1) into LDS, zero-filled outside the detector, so each tap is an
@@ -792,19 +801,40 @@ __device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j
 // VB-vector of samples (32 B for 8 float nodes) is split into 16-byte planes so
 // that lanes reading consecutive bins hit consecutive banks (no conflicts).
 // Two angles are processed per iteration to keep 4 LDS reads in flight.
-constexpr int kBTJ = 64;
-constexpr int kBTI = 4;
+// Tile kBTJ x kBTI, one pixel per thread, each wave a 16 (j) x 4 (i) patch.  The window
+// must hold the tile's projected extent, at most sqrt((kBTJ-1)^2 + (kBTI-1)^2) bins
+// (|Bi|, |Bj| <= 1 because the detector is never finer than the pixel), plus 3 bins of
+// floor / margin / second tap.  Bigger tiles stage one window for more pixels
+// (L2 traffic per tap ~ window / pixels).
+#ifndef ADMM_BK_TI
+#define ADMM_BK_TI 32
+#endif
+#ifndef ADMM_BK_TJ
+#define ADMM_BK_TJ 32
+#endif
+constexpr int kBTJ = ADMM_BK_TJ;
+constexpr int kBTI = ADMM_BK_TI;
+constexpr int kBkThreads = kBTJ * kBTI;
+constexpr int kBkWaves = kBkThreads / 64;
+constexpr int kBkPatchJ = kBTJ / 16;  // 16 x 4 wave patches per tile row
+static_assert((kBTJ == 32 || kBTJ == 64) && kBTI % 4 == 0 && kBkThreads <= 1024 && kBkWaves >= 4,
+              "unsupported back-projector tile");
+constexpr int ce_isqrt_ceil(int v) {
+  int r = 0;
+  while (r * r < v) ++r;
+  return r;
+}
+constexpr int kBWin = ((ce_isqrt_ceil((kBTJ - 1) * (kBTJ - 1) + (kBTI - 1) * (kBTI - 1)) + 3 + 7) / 8) * 8;
 #ifndef ADMM_BK_ANGC
-#define ADMM_BK_ANGC 16
+#define ADMM_BK_ANGC 32
 #endif
 constexpr int kBAngC = ADMM_BK_ANGC;  // angles per staged sinogram-window chunk
-constexpr int kBWin = 72;
 
 #ifndef ADMM_BK_EXPT
 #define ADMM_BK_EXPT 0  // timing diagnostics only: 1 = no angle loop, 2 = no window loads, 3 = no H epilogue
 #endif
 template <typename T, int VB, int MODE>
-__global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
+__global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
   constexpr int NQ = (MODE == BACK_H) ? 5 : (MODE == BACK_DIAG) ? 4 : 1;
   constexpr int NPL = Planes<T, VB>::NPL, PV = Planes<T, VB>::PV;
   const int N = A.N, n_det = A.n_det, n_ang = A.n_ang;
@@ -812,9 +842,9 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
   const int jb = blockIdx.x * kBTJ, ib = blockIdx.y * kBTI;
   // each wave covers a 16 (j) x 4 (i) patch: a 16-lane ds_read_b128 group then spans
   // <= ~16 detector bins for any angle (64 x 1 rows spanned up to 27 -> bank conflicts)
-  const int lane = threadIdx.x & 63;
-  const int j = jb + 16 * (threadIdx.x >> 6) + (lane & 15);
-  const int i = ib + (lane >> 4);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int j = jb + 16 * (wv % kBkPatchJ) + (lane & 15);
+  const int i = ib + 4 * (wv / kBkPatchJ) + (lane >> 4);
   const bool inb = (i < N) && (j < N);
   const int chunk = blockIdx.z;
   const int v0 = chunk * VB;
@@ -826,8 +856,11 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
   const int jhi = min(jb + kBTJ - 1, N - 1), ihi = min(ib + kBTI - 1, N - 1);
   const double Kc = A.K;
 
-  __shared__ Pack<T, PV> win[NPL][(MODE == BACK_WSQ) ? 1 : kBAngC][kBWin];
-  __shared__ int4 kmin_s[kBAngC / 4];
+  // angles per staged chunk: halved for 64-B sample vectors (8 float64 nodes) so the
+  // window stays at 48 KB of LDS
+  constexpr int ANGC = (NPL > 2) ? kBAngC / 2 : kBAngC;
+  __shared__ Pack<T, PV> win[NPL][(MODE == BACK_WSQ) ? 1 : ANGC][kBWin];
+  __shared__ int4 kmin_s[ANGC / 4];
   T acc[VB];
 #pragma unroll
   for (int u = 0; u < VB; ++u) acc[u] = T(0);
@@ -875,8 +908,8 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
     }
   };
 
-  for (int t0 = 0; t0 < n_ang; t0 += kBAngC) {
-    const int nt = min(kBAngC, n_ang - t0);
+  for (int t0 = 0; t0 < n_ang; t0 += ANGC) {
+    const int nt = min(ANGC, n_ang - t0);
     if constexpr (MODE != BACK_WSQ) {
       __syncthreads();
       if ((int)threadIdx.x < nt) {
@@ -886,7 +919,7 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
         reinterpret_cast<int*>(kmin_s)[threadIdx.x] = (int)floor(kmn) - 1;
       }
       __syncthreads();
-      for (int q = threadIdx.x; q < nt * kBWin * NPL; q += kBlock) {
+      for (int q = threadIdx.x; q < nt * kBWin * NPL; q += kBkThreads) {
         const int pl = q % NPL, aw = q / NPL;
         const int a = aw / kBWin, w = aw - a * kBWin;
         const int k = reinterpret_cast<const int*>(kmin_s)[a] + w;
@@ -949,7 +982,7 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
 
   if constexpr (MODE == BACK_H || MODE == BACK_DIAG) {
     constexpr int NV = ((VB * NQ + 15) / 16) * 16;
-    __shared__ double lds[4 * NV];
+    __shared__ double lds[kBkWaves * NV];
     __shared__ double tot[NV];
     double flat[NV];
 #pragma unroll
@@ -958,7 +991,7 @@ __global__ __launch_bounds__(kBlock) void k_back(BackArgs<T> A) {
     for (int u = 0; u < VB; ++u)
 #pragma unroll
       for (int q = 0; q < NQ; ++q) flat[u * NQ + q] = pq[u][q];
-    block_reduce_rs<NV>(flat, lds, tot);
+    block_reduce_rs<NV, kBkWaves>(flat, lds, tot);
     const int t = threadIdx.x;
     if (t < VB * NQ && t / NQ < nv) {
       const int P = gridDim.x * gridDim.y;
