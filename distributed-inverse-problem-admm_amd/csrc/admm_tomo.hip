@@ -74,8 +74,12 @@ struct admm_ctx {
   BackAngle* bang = nullptr;
   BackAngleC* bangc = nullptr;
   double Kb = 0.0;  // angle-independent part of the back projector's k_f
-  FgGroup* groups = nullptr;  // angle groups of the grouped forward projector
+  FgGroup* groups = nullptr;  // angle groups of the grouped forward projector (active plan)
   int n_groups = 0;           // 0: geometry does not fit the grouped kernel -> k_fwd
+  int fg_nkc = 0;             // grid.x of the grouped kernel: most chunks of any (group, segment)
+  // the two group plans (0: unaligned, 1: ray-aligned per row segment), chosen at bind time
+  FgGroup* plan_groups[2] = {nullptr, nullptr};
+  int plan_n[2] = {0, 0}, plan_nkc[2] = {0, 0}, plan_blocks[2] = {0, 0};
   hipStream_t cap = nullptr;  // private capture stream
 
   // operator-API scratch
@@ -97,6 +101,37 @@ struct admm_ctx {
 namespace {
 
 int vb_for(int V) { return V >= 5 ? 8 : (V >= 3 ? 4 : (V == 2 ? 2 : 1)); }
+
+void select_fwd_plan(admm_ctx* C, int pl) {
+  C->groups = C->plan_groups[pl];
+  C->n_groups = C->plan_n[pl];
+  C->fg_nkc = C->plan_nkc[pl];
+}
+
+// Forward plan for the bound batch: the ray-aligned plan stages less per tap but has one
+// more chunk per (group, segment); take it unless the busiest CU would host more of its
+// blocks (e.g. 512^2: 512 unaligned blocks put 2 on every one of 256 CUs, the aligned 528
+// put 3 on some; co-resident blocks share the CU).  ADMM_FWD_PLAN=0/1 forces a plan.
+// (The occupancy query only guards against a plan that cannot be resident at all.)
+template <typename T, int VB>
+int choose_fwd_plan(admm_ctx* C, int V) {
+  if (C->plan_n[0] == 0) return ADMM_OK;
+  int per_cu = 0, cus = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fwdg<T, VB>, kFgThreads, 0));
+  HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, C->device));
+  if (per_cu < 1) return fail(ADMM_E_HIP, "grouped forward projector cannot be resident");
+  const long nch = (V + VB - 1) / VB;
+  auto per_cu_max = [&](int pl) { return ((long)C->plan_blocks[pl] * nch + cus - 1) / std::max(1, cus); };
+  int pl = per_cu_max(1) <= per_cu_max(0) ? 1 : 0;
+  const char* f = getenv("ADMM_FWD_PLAN");
+  if (f && (f[0] == '0' || f[0] == '1')) pl = f[0] - '0';
+  if (getenv("ADMM_DEBUG_PLAN"))
+    fprintf(stderr, "[admm] forward plans: unaligned %d groups %d blocks, aligned %d groups %d blocks, "
+                    "x%ld chunks, %d CUs -> %s\n", C->plan_n[0], C->plan_blocks[0], C->plan_n[1],
+            C->plan_blocks[1], nch, cus, pl ? "aligned" : "unaligned");
+  select_fwd_plan(C, pl);
+  return ADMM_OK;
+}
 
 template <typename F>
 int with_vb(int vb, F&& f) {
@@ -128,7 +163,7 @@ int launch_fwd(admm_ctx* C, const T* img, const T* imgT, T* sino, const T* b, do
 template <typename T, int VB>
 int launch_fwdg_taps(admm_ctx* C, const T* img, const T* imgT, int V, hipStream_t s) {
   const int nch = (V + VB - 1) / VB;
-  dim3 grid((C->g.n_det + 63) / 64, C->n_groups, nch * kFgSeg);
+  dim3 grid(C->fg_nkc, C->n_groups, nch * kFgSeg);
   hipLaunchKernelGGL((k_fwdg<T, VB>), grid, dim3(kFgThreads), 0, s, img, imgT, (T*)C->fpart.p, C->fang, C->groups,
                      C->g.N, C->g.n_det, C->g.n_angles, V);
   CHECK_LAUNCH();
@@ -413,42 +448,78 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
     bc[t].pad = 0.f;
   }
   // angle groups for the grouped forward projector: consecutive angles of one case,
-  // G <= kFgG, such that the union row window of a 64-ray chunk fits kFgWin (float64,
-  // same formulas as the device; 2 pixels of margin).
-  std::vector<FgGroup> groups;
+  // G <= kFgG, whose union row window of every 64-ray chunk fits kFgWin (float64, same
+  // formulas as the device; 2 pixels of margin).  Two plans: plain 64-ray chunks, and rays
+  // aligned per row segment (FgGroup.delta: narrower windows and larger groups, at the
+  // price of one more chunk per segment); admm_batch_bind picks one (fewer block rounds).
+  std::vector<FgGroup> groups_plan[2];
   bool fits = true;
+  int plan_nkc[2] = {0, 0}, plan_blocks[2] = {0, 0};
   {
-    const int nkc = (g.n_det + 63) / 64;
-    auto width_ok = [&](int t0, int G) {
+    const double cd = 0.5 * (g.n_det - 1);
+    auto plan_group = [&](int t0, int G, bool align, FgGroup& gr) -> bool {
       for (int q = 0; q < G; ++q)
         if (fa[t0 + q].caseA != fa[t0].caseA) return false;
-      for (int kc = 0; kc < nkc; ++kc) {
-        const int ks[2] = {kc * 64, std::min(kc * 64 + 63, g.n_det - 1)};
-        for (int m = 0; m < g.N; ++m) {
-          double lo = 1e300, hi = -1e300;
-          for (int q = 0; q < G; ++q)
-            for (int kk : ks) {
-              const double l = std::fma((double)m, fa[t0 + q].dl, std::fma((double)kk, fa[t0 + q].A1, fa[t0 + q].A0));
-              lo = std::min(lo, l);
-              hi = std::max(hi, l);
+      gr = FgGroup{};
+      gr.t0 = t0;
+      gr.G = G;
+      for (int s = 0; s < kFgSeg; ++s) {
+        const int mlo = s * g.N / kFgSeg, mhi = (s + 1) * g.N / kFgSeg;
+        const double mc = 0.5 * (mlo + mhi - 1);
+        const FwdAngle& r0 = fa[t0];
+        const double lref = r0.A0 + cd * r0.A1 + mc * r0.dl;  // reference ray at the centre row
+        int dmin = 0, dmax = 0;
+        for (int q = 0; q < G; ++q) {
+          const FwdAngle& b = fa[t0 + q];
+          const int d = align ? (int)std::lround((lref - b.A0 - cd * b.A1 - mc * b.dl) / b.A1) : 0;
+          gr.delta[s][q] = d;
+          dmin = std::min(dmin, d);
+          dmax = std::max(dmax, d);
+        }
+        const int kcb = (int)std::floor(-dmax / 64.0);
+        const int kce = (int)std::ceil((g.n_det - dmin) / 64.0);
+        gr.kcb[s] = kcb;
+        gr.nkc[s] = kce - kcb;
+        for (int kc = kcb; kc < kce; ++kc) {
+          for (int m = mlo; m < mhi; ++m) {
+            double lo = 1e300, hi = -1e300;
+            for (int q = 0; q < G; ++q) {
+              const FwdAngle& b = fa[t0 + q];
+              const int ka = std::max(kc * 64 + gr.delta[s][q], 0);
+              const int kb = std::min(kc * 64 + gr.delta[s][q] + 63, g.n_det - 1);
+              if (ka > kb) continue;
+              for (int kk : {ka, kb}) {
+                const double l = std::fma((double)m, b.dl, std::fma((double)kk, b.A1, b.A0));
+                lo = std::min(lo, l);
+                hi = std::max(hi, l);
+              }
             }
-          if (std::floor(hi) - std::floor(lo) + 2 > kFgWin - 2) return false;
+            if (lo > hi) continue;
+            if (std::floor(hi) - std::floor(lo) + 2 > kFgWin - 2) return false;
+          }
         }
       }
       return true;
     };
-    // greedy: the largest G <= kFgG consecutive same-case angles whose union window fits.
+    // greedy: the largest G <= kFgG consecutive same-case angles whose windows fit.
     // (Balanced splits of each same-case run were measured slower: they force wide windows
     // near 45 degrees, where greedy makes small narrow groups and stages fewer pixels.)
-    for (int t0 = 0; t0 < g.n_angles;) {
-      int G = std::min(kFgG, g.n_angles - t0);
-      while (G > 1 && !width_ok(t0, G)) --G;
-      if (G == 1 && !width_ok(t0, 1)) {
-        fits = false;
-        break;
+    for (int pl = 0; pl < 2 && fits; ++pl) {
+      for (int t0 = 0; t0 < g.n_angles;) {
+        int G = std::min(kFgG, g.n_angles - t0);
+        FgGroup gr{};
+        while (G > 1 && !plan_group(t0, G, pl == 1, gr)) --G;
+        if (G == 1 && !plan_group(t0, 1, pl == 1, gr)) {
+          fits = false;
+          break;
+        }
+        groups_plan[pl].push_back(gr);
+        for (int s = 0; s < kFgSeg; ++s) {
+          plan_nkc[pl] = std::max(plan_nkc[pl], gr.nkc[s]);
+          plan_blocks[pl] += gr.nkc[s];
+        }
+        t0 += G;
       }
-      groups.push_back(FgGroup{t0, G});
-      t0 += G;
     }
     if (getenv("ADMM_NO_FWDG") && getenv("ADMM_NO_FWDG")[0] == '1') fits = false;
   }
@@ -462,10 +533,16 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
   HIPCHK(hipMemcpy(C->bang, ba.data(), ba.size() * sizeof(BackAngle), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&C->bangc, bc.size() * sizeof(BackAngleC)));
   HIPCHK(hipMemcpy(C->bangc, bc.data(), bc.size() * sizeof(BackAngleC), hipMemcpyHostToDevice));
-  if (fits && !groups.empty()) {
-    HIPCHK(hipMalloc(&C->groups, groups.size() * sizeof(FgGroup)));
-    HIPCHK(hipMemcpy(C->groups, groups.data(), groups.size() * sizeof(FgGroup), hipMemcpyHostToDevice));
-    C->n_groups = (int)groups.size();
+  if (fits) {
+    for (int pl = 0; pl < 2; ++pl) {
+      const auto& gv = groups_plan[pl];
+      HIPCHK(hipMalloc(&C->plan_groups[pl], gv.size() * sizeof(FgGroup)));
+      HIPCHK(hipMemcpy(C->plan_groups[pl], gv.data(), gv.size() * sizeof(FgGroup), hipMemcpyHostToDevice));
+      C->plan_n[pl] = (int)gv.size();
+      C->plan_nkc[pl] = plan_nkc[pl];
+      C->plan_blocks[pl] = plan_blocks[pl];
+    }
+    select_fwd_plan(C, 0);  // until a batch is bound
   }
   HIPCHK(hipStreamCreateWithFlags(&C->cap, hipStreamNonBlocking));
   *out = C;
@@ -484,7 +561,8 @@ int admm_ctx_destroy(admm_ctx* C) {
   if (C->fang) (void)hipFree(C->fang);
   if (C->bang) (void)hipFree(C->bang);
   if (C->bangc) (void)hipFree(C->bangc);
-  if (C->groups) (void)hipFree(C->groups);
+  for (FgGroup* pg : C->plan_groups)
+    if (pg) (void)hipFree(pg);
   if (C->cap) (void)hipStreamDestroy(C->cap);
   delete C;
   return ADMM_OK;
@@ -585,6 +663,10 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   C->b = B;
   const int V = B.V;
   C->vb = vb_for(V);
+  RET(with_vb(C->vb, [&](auto vbc) {
+    constexpr int VB = decltype(vbc)::value;
+    return C->dtype == ADMM_DTYPE_F32 ? choose_fwd_plan<float, VB>(C, V) : choose_fwd_plan<double, VB>(C, V);
+  }));
   const size_t Vp = (size_t)((V + C->vb - 1) / C->vb) * C->vb;  // padded to whole chunks
   const size_t ds = dsize(C->dtype);
   RET(ensure(C->xs, Vp * npix * ds));

@@ -398,8 +398,16 @@ __device__ __forceinline__ int fg_ray_of_lane(int lane) {
   return (lane & 32) + r;
 }
 
+// One angle group of the grouped forward projector.  Within row segment s, angle t0+q's
+// rays are shifted by delta[s][q] so that every angle of the group crosses the same
+// pixels at the segment's centre row (the union row window then spans the 64 rays plus
+// the angular spread over half a segment, not over half the image); block x of segment s
+// covers rays (kcb[s] + x) * 64 + delta[s][q] + [0, 64) of angle t0+q.
 struct FgGroup {
   int t0, G;
+  int kcb[kFgSeg];          // first 64-ray chunk of each row segment (may be negative)
+  int nkc[kFgSeg];          // chunks of each row segment
+  int delta[kFgSeg][kFgG];  // per-angle ray offsets
 };
 
 template <typename T, int VB>
@@ -410,17 +418,19 @@ __global__ __launch_bounds__(kFgThreads) void k_fwdg(const T* __restrict__ img, 
   constexpr int NPL = Planes<T, VB>::NPL, PV = Planes<T, VB>::PV;
   constexpr int PER = (kFgRows * kFgWin * NPL + kFgThreads - 1) / kFgThreads;  // staged packs per thread
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int kc = blockIdx.x;
-  const FgGroup gr = groups[blockIdx.y];
+  const FgGroup* gr = groups + blockIdx.y;
   const int seg = blockIdx.z % kFgSeg, chunk = blockIdx.z / kFgSeg;
+  if ((int)blockIdx.x >= gr->nkc[seg]) return;  // block-uniform, before any barrier
+  const int G = gr->G, t0 = gr->t0;
+  const int kbase = (gr->kcb[seg] + (int)blockIdx.x) * 64;
   const int npix = N * N;
-  const int k = kc * 64 + fg_ray_of_lane(lane);
-  const int kcl = min(k, n_det - 1);
-  const int t = gr.t0 + min(g, gr.G - 1);
+  const int gq = min(g, G - 1);
+  const int k = kbase + gr->delta[seg][gq] + fg_ray_of_lane(lane);
+  const int kcl = clampi(k, 0, n_det - 1);
+  const int t = t0 + gq;
   const FwdAngle a = ang[t];
-  const T* src = (ang[gr.t0].caseA ? imgT : img) + (size_t)chunk * npix * VB;
+  const T* src = (ang[t0].caseA ? imgT : img) + (size_t)chunk * npix * VB;
   const double l0 = fma((double)kcl, a.A1, a.A0);
-  const int klo = kc * 64, khi = min(kc * 64 + 63, n_det - 1);
   const int m_lo = seg * N / kFgSeg, m_hi = (seg + 1) * N / kFgSeg;
   const int nrows = m_hi - m_lo;
 
@@ -431,15 +441,18 @@ __global__ __launch_bounds__(kFgThreads) void k_fwdg(const T* __restrict__ img, 
   for (int r = threadIdx.x; r < nrows; r += kFgThreads) {
     const double dm = (double)(m_lo + r);
     double lmin = 1e300, lmax = -1e300;
-    for (int gg = 0; gg < gr.G; ++gg) {
-      const FwdAngle b = ang[gr.t0 + gg];
-      const double la = fma(dm, b.dl, fma((double)klo, b.A1, b.A0));
-      const double lb = fma(dm, b.dl, fma((double)khi, b.A1, b.A0));
+    for (int gg = 0; gg < G; ++gg) {
+      const FwdAngle b = ang[t0 + gg];
+      const int ka = max(kbase + gr->delta[seg][gg], 0), kb = min(kbase + gr->delta[seg][gg] + 63, n_det - 1);
+      if (ka > kb) continue;  // no ray of this angle in the block
+      const double la = fma(dm, b.dl, fma((double)ka, b.A1, b.A0));
+      const double lb = fma(dm, b.dl, fma((double)kb, b.A1, b.A0));
       lmin = fmin(lmin, fmin(la, lb));
       lmax = fmax(lmax, fmax(la, lb));
     }
-    wlo_s[r] = (int)floor(lmin) - 1;
-    wnum_s[r] = min(kFgWin, (int)floor(lmax) - (int)floor(lmin) + 3);
+    const bool any = lmin <= lmax;  // always true for host-planned chunks
+    wlo_s[r] = any ? (int)floor(lmin) - 1 : 0;
+    wnum_s[r] = any ? min(kFgWin, (int)floor(lmax) - (int)floor(lmin) + 3) : 0;
   }
   __syncthreads();
 
@@ -524,7 +537,7 @@ __global__ __launch_bounds__(kFgThreads) void k_fwdg(const T* __restrict__ img, 
       }
     }
   }
-  if (g < gr.G && k < n_det) {
+  if (g < G && k >= 0 && k < n_det) {
     const size_t m_rays = (size_t)n_ang * n_det;
     gstore<T, VB>(part + (((size_t)seg * ((V + VB - 1) / VB) + chunk) * m_rays + (size_t)t * n_det + k) * VB, acc);
   }
