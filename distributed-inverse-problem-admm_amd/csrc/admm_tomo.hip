@@ -80,6 +80,9 @@ struct admm_ctx {
   // the two group plans (0: unaligned, 1: ray-aligned per row segment), chosen at bind time
   FgGroup* plan_groups[2] = {nullptr, nullptr};
   int plan_n[2] = {0, 0}, plan_nkc[2] = {0, 0}, plan_blocks[2] = {0, 0};
+  std::vector<FgGroup> plan_host[2];  // host copies (block table construction)
+  Buf fg_order;                       // int4 block table of the grouped forward projector
+  int fg_nblk = 0, fg_order_nch = 0;
   hipStream_t cap = nullptr;  // private capture stream
 
   // operator-API scratch
@@ -108,6 +111,37 @@ void select_fwd_plan(admm_ctx* C, int pl) {
   C->fg_nkc = C->plan_nkc[pl];
 }
 
+// Block table of the grouped forward projector for nch node chunks: every live
+// (ray chunk, group, segment, node chunk), sorted by group size G (waves of work), heaviest
+// first.  When every block is resident at once (<= 2 per CU) the second half is reversed so
+// the blocks sharing a CU pair heavy with light (dispatch fills one slot per CU, then the
+// second); otherwise heaviest-first is the longest-processing-time order.
+int build_fwd_order(admm_ctx* C, int pl, int nch, int cus) {
+  struct Blk {
+    int4 b;
+    int w;
+  };
+  std::vector<Blk> v;
+  const auto& gv = C->plan_host[pl];
+  for (int c = 0; c < nch; ++c)
+    for (int gi = 0; gi < (int)gv.size(); ++gi)
+      for (int s = 0; s < kFgSeg; ++s)
+        for (int kc = 0; kc < gv[gi].nkc[s]; ++kc) v.push_back({make_int4(kc, gi, s + kFgSeg * c, 0), gv[gi].G});
+  const int n = (int)v.size();
+  if (cus > 0) {  // cus <= 0: launch order = table order (tuning comparison)
+    std::stable_sort(v.begin(), v.end(), [](const Blk& a, const Blk& b) { return a.w > b.w; });
+    if (n <= 2 * cus && n > cus) std::reverse(v.begin() + cus, v.end());
+  }
+  std::vector<int4> t(n);
+  for (int i = 0; i < n; ++i) t[i] = v[i].b;
+  const int rc = ensure(C->fg_order, (size_t)n * sizeof(int4));
+  if (rc != ADMM_OK) return rc;
+  HIPCHK(hipMemcpy(C->fg_order.p, t.data(), (size_t)n * sizeof(int4), hipMemcpyHostToDevice));
+  C->fg_nblk = n;
+  C->fg_order_nch = nch;
+  return ADMM_OK;
+}
+
 // Forward plan for the bound batch: the ray-aligned plan stages less per tap but has one
 // more chunk per (group, segment); take it unless the busiest CU would host more of its
 // blocks (e.g. 512^2: 512 unaligned blocks put 2 on every one of 256 CUs, the aligned 528
@@ -130,7 +164,9 @@ int choose_fwd_plan(admm_ctx* C, int V) {
                     "x%ld chunks, %d CUs -> %s\n", C->plan_n[0], C->plan_blocks[0], C->plan_n[1],
             C->plan_blocks[1], nch, cus, pl ? "aligned" : "unaligned");
   select_fwd_plan(C, pl);
-  return ADMM_OK;
+  return getenv("ADMM_FWD_NATURAL_ORDER") && getenv("ADMM_FWD_NATURAL_ORDER")[0] == '1'
+             ? build_fwd_order(C, pl, (int)nch, 0)
+             : build_fwd_order(C, pl, (int)nch, cus);
 }
 
 template <typename F>
@@ -163,9 +199,9 @@ int launch_fwd(admm_ctx* C, const T* img, const T* imgT, T* sino, const T* b, do
 template <typename T, int VB>
 int launch_fwdg_taps(admm_ctx* C, const T* img, const T* imgT, int V, hipStream_t s) {
   const int nch = (V + VB - 1) / VB;
-  dim3 grid(C->fg_nkc, C->n_groups, nch * kFgSeg);
-  hipLaunchKernelGGL((k_fwdg<T, VB>), grid, dim3(kFgThreads), 0, s, img, imgT, (T*)C->fpart.p, C->fang, C->groups,
-                     C->g.N, C->g.n_det, C->g.n_angles, V);
+  if (nch != C->fg_order_nch) return fail(ADMM_E_STATE, "forward block table built for another batch size");
+  hipLaunchKernelGGL((k_fwdg<T, VB>), dim3(C->fg_nblk), dim3(kFgThreads), 0, s, img, imgT, (T*)C->fpart.p, C->fang,
+                     C->groups, (const int4*)C->fg_order.p, C->g.N, C->g.n_det, C->g.n_angles, V);
   CHECK_LAUNCH();
   return ADMM_OK;
 }
@@ -538,6 +574,7 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
       const auto& gv = groups_plan[pl];
       HIPCHK(hipMalloc(&C->plan_groups[pl], gv.size() * sizeof(FgGroup)));
       HIPCHK(hipMemcpy(C->plan_groups[pl], gv.data(), gv.size() * sizeof(FgGroup), hipMemcpyHostToDevice));
+      C->plan_host[pl] = gv;
       C->plan_n[pl] = (int)gv.size();
       C->plan_nkc[pl] = plan_nkc[pl];
       C->plan_blocks[pl] = plan_blocks[pl];
@@ -555,7 +592,7 @@ int admm_ctx_destroy(admm_ctx* C) {
   (void)hipDeviceSynchronize();
   free_graphs(C);
   Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->bI, &C->fpart, &C->r, &C->c,
-                 &C->d2, &C->e2, &C->partH, &C->partS, &C->partD, &C->partE, &C->redH};
+                 &C->d2, &C->e2, &C->partH, &C->partS, &C->partD, &C->partE, &C->redH, &C->fg_order};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (C->fang) (void)hipFree(C->fang);

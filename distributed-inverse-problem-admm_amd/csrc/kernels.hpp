@@ -413,16 +413,20 @@ struct FgGroup {
 template <typename T, int VB>
 __global__ __launch_bounds__(kFgThreads) void k_fwdg(const T* __restrict__ img, const T* __restrict__ imgT,
                                                  T* __restrict__ part, const FwdAngle* __restrict__ ang,
-                                                 const FgGroup* __restrict__ groups, int N, int n_det, int n_ang,
-                                                 int V) {
+                                                 const FgGroup* __restrict__ groups, const int4* __restrict__ order,
+                                                 int N, int n_det, int n_ang, int V) {
   constexpr int NPL = Planes<T, VB>::NPL, PV = Planes<T, VB>::PV;
   constexpr int PER = (kFgRows * kFgWin * NPL + kFgThreads - 1) / kFgThreads;  // staged packs per thread
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const FgGroup* gr = groups + blockIdx.y;
-  const int seg = blockIdx.z % kFgSeg, chunk = blockIdx.z / kFgSeg;
-  if ((int)blockIdx.x >= gr->nkc[seg]) return;  // block-uniform, before any barrier
+  // 1-D grid over a host-ordered block table (order[b] = {chunk of rays, group, seg +
+  // kFgSeg * node chunk}): heavy (large-G) blocks first, paired with light ones on a CU
+  const int4 ob = order[blockIdx.x];
+  const int bkc = ob.x;
+  const FgGroup* gr = groups + ob.y;
+  const int seg = ob.z % kFgSeg, chunk = ob.z / kFgSeg;
+  if (bkc >= gr->nkc[seg]) return;  // block-uniform, before any barrier (never in the table)
   const int G = gr->G, t0 = gr->t0;
-  const int kbase = (gr->kcb[seg] + (int)blockIdx.x) * 64;
+  const int kbase = (gr->kcb[seg] + bkc) * 64;
   const int npix = N * N;
   const int gq = min(g, G - 1);
   const int k = kbase + gr->delta[seg][gq] + fg_ray_of_lane(lane);
