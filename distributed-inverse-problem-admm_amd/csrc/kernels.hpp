@@ -410,8 +410,12 @@ struct FgGroup {
   int delta[kFgSeg][kFgG];  // per-angle ray offsets
 };
 
+#ifndef ADMM_FG_WPE
+#define ADMM_FG_WPE 8  // waves per SIMD the register budget must allow: <= 64 VGPRs, 2 blocks/CU
+                       // (float64 samples otherwise take 67 and fall to one block per CU)
+#endif
 template <typename T, int VB>
-__global__ __launch_bounds__(kFgThreads) void k_fwdg(const T* __restrict__ img, const T* __restrict__ imgT,
+__global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM_FG_WPE))) void k_fwdg(const T* __restrict__ img, const T* __restrict__ imgT,
                                                  T* __restrict__ part, const FwdAngle* __restrict__ ang,
                                                  const FgGroup* __restrict__ groups, const int4* __restrict__ order,
                                                  int N, int n_det, int n_ang, int V) {
