@@ -93,6 +93,7 @@ struct admm_ctx {
   admm_batch b{};
   int vb = 1;  // node interleave width of the sample buffers
   Buf xs, xsT, p, pT, Hp, sino, bI, fpart, r, c, d2, e2;
+  Buf dsumS;  // D = sum_j q_ij as interleaved samples (BACK_H epilogue)
   Buf partH, partS, partD, partE;
   Buf redH;
   int P_back = 0, P_tile = 0, P_fwd = 0, P_edge = 0;
@@ -272,6 +273,10 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
   const dim3 cgg((N + kTile - 1) / kTile, (N + kCgRows - 1) / kCgRows, nch);
   const int Pb = C->P_back;
 
+  // 0. D as interleaved samples for the CG operator (D is setup data; repacked per update)
+  hipLaunchKernelGGL((k_pack_d<T, VB>), dim3((unsigned)((npix + 255) / 256), nch), dim3(256), 0, s, B.dsum,
+                     (T*)C->dsumS.p, (int)npix, V);
+  CHECK_LAUNCH();
   // 1. neighbour gather: c = sum_j q_ij (z_ij - y_ij,i); xs = (T) x (+ transpose)
   hipLaunchKernelGGL((k_gather<T, VB>), tg, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.q, B.inc_off, B.inc_edge,
                      B.inc_qslot, B.inc_sign, B.fusion == ADMM_FUSE_WEIGHTED ? B.y_b : nullptr, c, xs, xsT,
@@ -314,6 +319,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
       a.pin = p;
       a.r = r;
       a.dsum = B.dsum;
+      a.dsum_s = (const T*)C->dsumS.p;
       a.rho = B.rho;
       a.lam = B.lam;
       a.mu = B.mu;
@@ -592,7 +598,7 @@ int admm_ctx_destroy(admm_ctx* C) {
   (void)hipDeviceSynchronize();
   free_graphs(C);
   Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->bI, &C->fpart, &C->r, &C->c,
-                 &C->d2, &C->e2, &C->partH, &C->partS, &C->partD, &C->partE, &C->redH, &C->fg_order};
+                 &C->d2, &C->e2, &C->partH, &C->partS, &C->partD, &C->partE, &C->redH, &C->fg_order, &C->dsumS};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (C->fang) (void)hipFree(C->fang);
@@ -711,6 +717,7 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   RET(ensure(C->p, Vp * npix * ds));
   RET(ensure(C->pT, Vp * npix * ds));
   RET(ensure(C->Hp, Vp * npix * ds));
+  RET(ensure(C->dsumS, Vp * npix * ds));
   RET(ensure(C->sino, Vp * m * ds));
   RET(ensure(C->bI, Vp * m * ds));
   if (C->n_groups > 0) RET(ensure(C->fpart, (size_t)kFgSeg * Vp * m * ds));

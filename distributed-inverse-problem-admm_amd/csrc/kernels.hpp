@@ -631,6 +631,7 @@ struct BackArgs {
   const T* pin;             // H: p;  INIT: xs (interleaved)
   const double* r;          // H: r
   const double* dsum;       // [V][n]
+  const T* dsum_s;          // H: D as interleaved samples [C][n][VB] (one VB-vector per pixel)
   const double* atb;        // INIT
   const double* cvec;       // INIT, DIAG: c = sum_j q v
   const double* dvar;       // INIT: d [V][2][n]
@@ -739,14 +740,18 @@ __device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j
 #pragma unroll
       for (int u = 0; u < VB; ++u) ktk[u] -= (double)pn[u] - (double)pc[u];
     }
-    T outv[VB];
+    T outv[VB], dv[VB];
+    // H: D read as one sample vector (float64 D rounded to T: a 2^-24-relative change of the
+    // rho D p term, far below the float32 Hp it produces); INIT keeps float64 D
+    if constexpr (MODE == BACK_H) gload<T, VB>(A.dsum_s + sbase + (size_t)pix * VB, dv);
 #pragma unroll
     for (int u = 0; u < VB; ++u) {
       outv[u] = T(0);
       if (u < nv) {
         const size_t vo = (size_t)(v0 + u) * npix;
         const double pcd = (double)pc[u];
-        const double h = (double)acc[u] + A.rho * A.dsum[vo + pix] * pcd + A.mu * ktk[u];
+        const double dd = (MODE == BACK_H) ? (double)dv[u] : A.dsum[vo + pix];
+        const double h = (double)acc[u] + A.rho * dd * pcd + A.mu * ktk[u];
         if constexpr (MODE == BACK_H) {
           const T hp = (T)h;
           outv[u] = hp;
@@ -1324,6 +1329,18 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
     tl.t[rw][mp.jj][mp.u] = sv;
   }
   tile_store_T<T, VB>(tl, pT + sbase, N, i0, j0);
+}
+
+// node-major float64 [V][L] -> interleaved samples [C][L][VB] of type T  (grid.y = chunk)
+template <typename T, int VB>
+__global__ void k_pack_d(const double* __restrict__ in, T* __restrict__ out, int L, int V) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  const int chunk = blockIdx.y, v0 = chunk * VB;
+  if (q >= L) return;
+  T s[VB];
+#pragma unroll
+  for (int u = 0; u < VB; ++u) s[u] = (v0 + u < V) ? (T)in[(size_t)(v0 + u) * L + q] : T(0);
+  gstore<T, VB>(out + ((size_t)chunk * L + q) * VB, s);
 }
 
 // node-major [V][L] samples -> interleaved [C][L][VB]  (grid.y = chunk)
