@@ -459,8 +459,13 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       lmax = fmax(lmax, fmax(la, lb));
     }
     const bool any = lmin <= lmax;  // always true for host-planned chunks
-    wlo_s[r] = any ? (int)floor(lmin) - 1 : 0;
-    wnum_s[r] = any ? min(kFgWin, (int)floor(lmax) - (int)floor(lmin) + 3) : 0;
+    // even window origin: a tap's even/odd LDS half, and so the order of a ray's two FMAs
+    // per row, then follows the absolute pixel parity -- identical for every group / ray
+    // layout / block order, so results do not depend on the plan (or on the GPU count that
+    // chooses it).  The one extra column fits the host's 2-pixel window margin.
+    const int wlo = ((int)floor(lmin) - 1) & ~1;
+    wlo_s[r] = any ? wlo : 0;
+    wnum_s[r] = any ? min(kFgWin, (int)floor(lmax) - wlo + 2) : 0;
   }
   __syncthreads();
 
