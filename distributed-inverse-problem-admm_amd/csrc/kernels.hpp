@@ -387,6 +387,9 @@ constexpr int kFgG = ADMM_FG_G;        // max angles (waves) per block
 constexpr int kFgThreads = 64 * kFgG;
 constexpr int kFgWin = ADMM_FG_WIN;    // staged window width (pixels)
 constexpr int kFgSeg = ADMM_FG_SEG;    // row segments (partial sums) per ray
+#ifndef ADMM_FG_EO
+#define ADMM_FG_EO 1  // even/odd half-window LDS layout (0: plain pixel order, tuning only)
+#endif
 constexpr int kFgHalf = kFgWin / 2;        // slots per parity
 constexpr int kFgOdd = kFgHalf + 4;        // odd half-window offset (+64 B bank shift)
 constexpr int kFgRow = kFgOdd + kFgHalf;   // 16-B slots per staged row and plane
@@ -496,7 +499,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       if (q < kFgRows * kFgWin * NPL) {
         const int pl = q % NPL, rw = q / NPL;
         const int r = rw / kFgWin, w = rw - r * kFgWin;
-        win[pl][r][(w & 1) ? kFgOdd + (w >> 1) : (w >> 1)] = stage[e];
+        win[pl][r][ADMM_FG_EO ? ((w & 1) ? kFgOdd + (w >> 1) : (w >> 1)) : w] = stage[e];
       }
     }
   };
@@ -535,9 +538,20 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       }
       const T w0 = T(1) - w1;
       // taps idx (weight w0) and idx+1 (w1): one is even, one odd
-      const bool odd = idx & 1;
-      const int se = (idx + 1) >> 1, so = kFgOdd + (idx >> 1);
-      const T we = odd ? w1 : w0, wo = odd ? w0 : w1;
+      int se, so;
+      T we, wo;
+      if constexpr (ADMM_FG_EO) {
+        const bool odd = idx & 1;
+        se = (idx + 1) >> 1;
+        so = kFgOdd + (idx >> 1);
+        we = odd ? w1 : w0;
+        wo = odd ? w0 : w1;
+      } else {  // plain layout (tuning comparison): left tap, then right tap
+        se = idx;
+        so = idx + 1;
+        we = w0;
+        wo = w1;
+      }
 #pragma unroll
       for (int q = 0; q < NPL; ++q) {
         const Pack<T, PV> s0 = win[q][r][se];
