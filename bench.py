@@ -185,7 +185,7 @@ def main():
                      make_sinograms([ops[g] for g in plan.local_nodes], ph, 0.005, seed=1000 + lo)))
     Wi, Q = make_precisions(ops)  # one W kernel launch: every node shares the geometry
     nb = NodeBatch(geom, dtype, plan, sinos, Q, RHO, LAM, 10 * LAM, TV_ITERS, CG_ITERS, tv_kind,
-                   ph, local_rank)
+                   ph, local_rank, keep_x=True)
     halo = HaloExchange(plan, nb.x_ext)
     if world > 1:
         dist.barrier()

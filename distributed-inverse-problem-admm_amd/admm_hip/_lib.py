@@ -19,6 +19,7 @@ ADMM_TV_ISO = 0
 ADMM_TV_ANISO = 1
 ADMM_FUSE_MIDPOINT = 0
 ADMM_FUSE_WEIGHTED = 1
+ADMM_BATCH_KEEP_X = 1  # admm_batch.flags: x_ext local rows written only by admm_node_update
 ABI_VERSION = 2
 ADMM_MASK_KNN = 0
 ADMM_MASK_MST = 1
@@ -81,7 +82,7 @@ class Batch(C.Structure):
         ("node_stats", C.c_void_p),
         ("edge_stats", C.c_void_p),
         ("fusion", C.c_int32),
-        ("reserved2", C.c_int32),
+        ("flags", C.c_int32),
         ("y_b", C.c_void_p),
         ("w", C.c_void_p),
     ]

@@ -89,7 +89,8 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
     if snapshot_every is None:
         snapshot_every = max(1, max_iters // snapshot_div)  # _ver2:31-32
     nb = NodeBatch(geom, dtype, plan, sinograms, Qij_diag_fn, rho, lam_tv, mu, tv_iters, cg_iters,
-                   tv_kind, phantom_true, device, fusion=fusion, Wi_list=Wi_list)
+                   tv_kind, phantom_true, device, fusion=fusion, Wi_list=Wi_list,
+                   keep_x=True)  # this loop never writes x itself
     halo = HaloExchange(plan, nb.x_ext, group)
     if world > 1:
         dist.barrier(group=group)

@@ -9,7 +9,9 @@ Holds, in HBM, everything one GPU needs for its graph nodes (layout: DESIGN.md
   (admm_consensus; replaces block_6_admm_loop_ver2.py:210-253).
 
 Both are stream-ordered on the current torch stream and replay hipGraphs
-recorded at bind time.
+recorded at bind time.  ``keep_x=True`` promises that nothing but ``node_update``
+writes the local rows of ``x_ext``; each update then starts from the previous
+update's A^T(Ax - b) instead of projecting x again (ADMM_BATCH_KEEP_X).
 """
 from __future__ import annotations
 
@@ -41,7 +43,7 @@ class NodeBatch:
     def __init__(self, geom: ParallelBeamGeometry, dtype: str, plan: ShardPlan, sinograms,
                  Qij_diag_fn, rho: float, lam: float, mu: float, tv_iters: int = 10,
                  cg_iters: int = 5, tv_kind: str = "iso", phantom=None, device: int = 0,
-                 fusion: str = "midpoint", Wi_list=None):
+                 fusion: str = "midpoint", Wi_list=None, keep_x: bool = False):
         self.lib = _lib.load()
         self.geom = geom
         self.plan = plan
@@ -129,7 +131,8 @@ class NodeBatch:
             p(self.y), p(self.z), p(self.q), p(self.edge_a), p(self.edge_b), p(self.inc_off),
             p(self.inc_edge), p(self.inc_qslot), p(self.inc_sign), p(self.node_stats),
             p(self.edge_stats),
-            _lib.ADMM_FUSE_WEIGHTED if fusion == "weighted" else _lib.ADMM_FUSE_MIDPOINT, 0,
+            _lib.ADMM_FUSE_WEIGHTED if fusion == "weighted" else _lib.ADMM_FUSE_MIDPOINT,
+            _lib.ADMM_BATCH_KEEP_X if keep_x else 0,
             p(self.y_b), p(self.w))
         torch.cuda.synchronize(dev)
         _lib.check(self.lib.admm_batch_bind(self.ctx.h, C.byref(self.cb)), "admm_batch_bind")

@@ -94,6 +94,10 @@ struct admm_ctx {
   int vb = 1;  // node interleave width of the sample buffers
   Buf xs, xsT, p, pT, Hp, sino, bI, fpart, r, c, d2, e2;
   Buf dsumS;  // D = sum_j q_ij as interleaved samples (BACK_H epilogue)
+  Buf ats;    // A^T (A xs - b) of the last update's final x (ADMM_BATCH_KEEP_X)
+  bool ats_valid = false;  // ats matches x_ext's local rows
+  hipGraph_t g_update_reuse = nullptr;
+  hipGraphExec_t x_update_reuse = nullptr;
   Buf partH, partS, partD, partE;
   Buf redH;
   int P_back = 0, P_tile = 0, P_fwd = 0, P_edge = 0;
@@ -255,7 +259,7 @@ int launch_reduce(const double* part, int rows, int P, double* out, int G, int o
 // the x-update sequence for the bound batch (replaces block_6_admm_loop_ver2.py:81-197)
 // --------------------------------------------------------------------------
 template <typename T, int VB>
-int enqueue_update(admm_ctx* C, hipStream_t s) {
+int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false) {
   const admm_batch& B = C->b;
   const int V = B.V, N = C->g.N;
   const size_t npix = (size_t)N * N;
@@ -283,6 +287,11 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
                      N, V);
   CHECK_LAUNCH();
   // 2-4. r = A^T b + rho c + mu K^T(d - e) - H x,  p = r,  rr
+  if (reuse) {  // A^T A xs from the previous update's diagnostics (ADMM_BATCH_KEEP_X)
+    hipLaunchKernelGGL((k_init_reuse<T, VB>), cgg, dim3(kBlock), 0, s, (const T*)C->ats.p, xs, B.atb, c, B.dsum,
+                       B.d, B.e, r, p, B.rho, B.mu, N, V);
+    CHECK_LAUNCH();
+  } else {
   RET((launch_fwd_batch<T, VB, 0>(C, xs, xsT, sino, nullptr, nullptr, V, s)));
   {
     BackArgs<T> a{};
@@ -299,6 +308,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
     a.lam = B.lam;
     a.mu = B.mu;
     RET((launch_back<T, VB, BACK_INIT>(C, a, V, s)));
+  }
   }
   hipLaunchKernelGGL((k_transpose<T, VB>), tg, dim3(kBlock), 0, s, p, pT, N);
   CHECK_LAUNCH();
@@ -367,6 +377,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
     a.lam = B.lam;
     a.mu = B.mu;
     a.tv_kind = B.tv_kind;
+    a.out_t = (B.flags & ADMM_BATCH_KEEP_X) ? (T*)C->ats.p : nullptr;
     RET((launch_back<T, VB, BACK_DIAG>(C, a, V, s)));
   }
   RET(launch_reduce((double*)C->partS.p, V, C->P_fwd, B.node_stats, 1, ADMM_NODE_STATS, ADMM_NODE_STAT_MSE_SINO, s));
@@ -375,8 +386,8 @@ int enqueue_update(admm_ctx* C, hipStream_t s) {
 }
 
 template <typename T>
-int enqueue_update_any(admm_ctx* C, hipStream_t s) {
-  return with_vb(C->vb, [&](auto vbc) { return enqueue_update<T, decltype(vbc)::value>(C, s); });
+int enqueue_update_any(admm_ctx* C, hipStream_t s, bool reuse = false) {
+  return with_vb(C->vb, [&](auto vbc) { return enqueue_update<T, decltype(vbc)::value>(C, s, reuse); });
 }
 
 int enqueue_consensus(admm_ctx* C, hipStream_t s) {
@@ -402,6 +413,10 @@ int free_graphs(admm_ctx* C) {
   if (C->g_cons) HIPCHK(hipGraphDestroy(C->g_cons));
   C->x_update = nullptr;
   C->g_update = nullptr;
+  if (C->x_update_reuse) HIPCHK(hipGraphExecDestroy(C->x_update_reuse));
+  if (C->g_update_reuse) HIPCHK(hipGraphDestroy(C->g_update_reuse));
+  C->x_update_reuse = nullptr;
+  C->g_update_reuse = nullptr;
   C->x_cons = nullptr;
   C->g_cons = nullptr;
   return ADMM_OK;
@@ -598,7 +613,7 @@ int admm_ctx_destroy(admm_ctx* C) {
   (void)hipDeviceSynchronize();
   free_graphs(C);
   Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->bI, &C->fpart, &C->r, &C->c,
-                 &C->d2, &C->e2, &C->partH, &C->partS, &C->partD, &C->partE, &C->redH, &C->fg_order, &C->dsumS};
+                 &C->d2, &C->e2, &C->partH, &C->partS, &C->partD, &C->partE, &C->redH, &C->fg_order, &C->dsumS, &C->ats};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (C->fang) (void)hipFree(C->fang);
@@ -694,6 +709,7 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
                         !B.inc_sign || !B.edge_stats))
     return fail(ADMM_E_INVALID, "null edge pointer");
   if (B.fusion != ADMM_FUSE_MIDPOINT && B.fusion != ADMM_FUSE_WEIGHTED) return fail(ADMM_E_INVALID, "bad fusion");
+  if (B.flags & ~ADMM_BATCH_KEEP_X) return fail(ADMM_E_INVALID, "unknown batch flags");
   if (B.fusion == ADMM_FUSE_WEIGHTED && B.n_edges > 0 && (!B.y_b || !B.w))
     return fail(ADMM_E_INVALID, "weighted fusion needs y_b and w");
   if (B.n_edges > 65535) return fail(ADMM_E_INVALID, "more than 65535 edge slots on one device");
@@ -718,6 +734,8 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   RET(ensure(C->pT, Vp * npix * ds));
   RET(ensure(C->Hp, Vp * npix * ds));
   RET(ensure(C->dsumS, Vp * npix * ds));
+  if (B.flags & ADMM_BATCH_KEEP_X) RET(ensure(C->ats, Vp * npix * ds));
+  C->ats_valid = false;
   RET(ensure(C->sino, Vp * m * ds));
   RET(ensure(C->bI, Vp * m * ds));
   if (C->n_groups > 0) RET(ensure(C->fpart, (size_t)kFgSeg * Vp * m * ds));
@@ -744,6 +762,13 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
       return C->dtype == ADMM_DTYPE_F32 ? enqueue_update_any<float>(C, s) : enqueue_update_any<double>(C, s);
     };
     RET(capture(C, fu, &C->g_update, &C->x_update));
+    if (B.flags & ADMM_BATCH_KEEP_X) {
+      auto fr = [&](hipStream_t s) {
+        return C->dtype == ADMM_DTYPE_F32 ? enqueue_update_any<float>(C, s, true)
+                                          : enqueue_update_any<double>(C, s, true);
+      };
+      RET(capture(C, fr, &C->g_update_reuse, &C->x_update_reuse));
+    }
     if (B.n_edges > 0) {
       auto fc = [&](hipStream_t s) { return enqueue_consensus(C, s); };
       RET(capture(C, fc, &C->g_cons, &C->x_cons));
@@ -781,11 +806,17 @@ int admm_batch_atb(admm_ctx* C, double* atb_out, void* stream) {
 int admm_node_update(admm_ctx* C, void* stream) {
   if (!C || !C->bound) return fail(ADMM_E_STATE, "no batch bound");
   hipStream_t s = (hipStream_t)stream;
+  const bool keep = (C->b.flags & ADMM_BATCH_KEEP_X) != 0;
+  const bool reuse = keep && C->ats_valid;
+  int rc = ADMM_OK;
   if (C->x_update) {
-    HIPCHK(hipGraphLaunch(C->x_update, s));
-    return ADMM_OK;
+    HIPCHK(hipGraphLaunch(reuse ? C->x_update_reuse : C->x_update, s));
+  } else {
+    rc = C->dtype == ADMM_DTYPE_F32 ? enqueue_update_any<float>(C, s, reuse)
+                                    : enqueue_update_any<double>(C, s, reuse);
   }
-  return C->dtype == ADMM_DTYPE_F32 ? enqueue_update_any<float>(C, s) : enqueue_update_any<double>(C, s);
+  if (rc == ADMM_OK && keep) C->ats_valid = true;  // this update's DIAG left A^T s of its x
+  return rc;
 }
 
 int admm_consensus(admm_ctx* C, void* stream) {

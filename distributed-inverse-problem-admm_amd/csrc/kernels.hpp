@@ -792,6 +792,9 @@ __device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j
     }
     gstore<T, VB>(A.out_t + sbase + (size_t)pix * VB, outv);
   } else if constexpr (MODE == BACK_DIAG) {
+    // A^T s = A^T (A xs - b) of the final x: kept (out_t != null) so the next x-update
+    // can start without projecting x again (k_init_reuse)
+    if (A.out_t) gstore<T, VB>(A.out_t + sbase + (size_t)pix * VB, acc);
 #pragma unroll
     for (int u = 0; u < VB; ++u) {
       if (u >= nv) continue;
@@ -1079,6 +1082,69 @@ __device__ __forceinline__ void tile_store_T(TileT<T, VB>& tl, T* __restrict__ o
     const int jj = j0 + c, ii = i0 + r;
     if (jj < N && ii < N) outT[((size_t)jj * N + ii) * VB + u] = tl.t[r][c][u];
   }
+}
+
+// CG start from the previous x-update's diagnostics (batch flag ADMM_BATCH_KEEP_X: x_ext's
+// local rows were last written by admm_node_update).  The previous DIAG left
+// ats = A^T (A xs - b) for this very xs, so A^T A xs = ats + A^T b needs no projection:
+//   r = A^T b + rho c + mu K^T (d - e) - (ats + A^T b + rho D xs + mu K^T K xs),  p = r
+// (BACK_INIT's epilogue with its projected A^T A xs replaced).  One thread per pixel,
+// all VB nodes of the chunk; (kBlock / kTile) x kTile pixels per block (the CG update's grid).
+template <typename T, int VB>
+__global__ __launch_bounds__(kBlock) void k_init_reuse(const T* __restrict__ ats, const T* __restrict__ xs,
+                                                       const double* __restrict__ atb,
+                                                       const double* __restrict__ cvec,
+                                                       const double* __restrict__ dsum, const double* __restrict__ dvar,
+                                                       const double* __restrict__ evar, double* __restrict__ r,
+                                                       T* __restrict__ p, double rho, double mu, int N, int V) {
+  const int chunk = blockIdx.z, v0 = chunk * VB, nv = min(VB, V - v0);
+  const int npix = N * N;
+  const size_t sbase = (size_t)chunk * npix * VB;
+  const int jj = threadIdx.x % kTile, ii = threadIdx.x / kTile;
+  const int i = blockIdx.y * (kBlock / kTile) + ii, j = blockIdx.x * kTile + jj;
+  if (i >= N || j >= N) return;
+  const int pix = i * N + j;
+  const T* pv = xs + sbase;
+  T pc[VB], pn[VB], av[VB];
+  double ktk[VB];
+  gload<T, VB>(pv + (size_t)pix * VB, pc);
+  gload<T, VB>(ats + sbase + (size_t)pix * VB, av);
+#pragma unroll
+  for (int u = 0; u < VB; ++u) ktk[u] = 0.0;
+  if (i >= 1) {
+    gload<T, VB>(pv + (size_t)(pix - N) * VB, pn);
+#pragma unroll
+    for (int u = 0; u < VB; ++u) ktk[u] += (double)pc[u] - (double)pn[u];
+  }
+  if (i <= N - 2) {
+    gload<T, VB>(pv + (size_t)(pix + N) * VB, pn);
+#pragma unroll
+    for (int u = 0; u < VB; ++u) ktk[u] -= (double)pn[u] - (double)pc[u];
+  }
+  if (j >= 1) {
+    gload<T, VB>(pv + (size_t)(pix - 1) * VB, pn);
+#pragma unroll
+    for (int u = 0; u < VB; ++u) ktk[u] += (double)pc[u] - (double)pn[u];
+  }
+  if (j <= N - 2) {
+    gload<T, VB>(pv + (size_t)(pix + 1) * VB, pn);
+#pragma unroll
+    for (int u = 0; u < VB; ++u) ktk[u] -= (double)pn[u] - (double)pc[u];
+  }
+  T outv[VB];
+#pragma unroll
+  for (int u = 0; u < VB; ++u) {
+    outv[u] = T(0);
+    if (u < nv) {
+      const size_t vo = (size_t)(v0 + u) * npix;
+      const double ab = atb[vo + pix];
+      const double h = ((double)av[u] + ab) + rho * dsum[vo + pix] * (double)pc[u] + mu * ktk[u];
+      const double rr = ab + rho * cvec[vo + pix] + mu * kt_w_at(dvar + 2 * vo, evar + 2 * vo, N, i, j) - h;
+      r[vo + pix] = rr;
+      outv[u] = (T)rr;
+    }
+  }
+  gstore<T, VB>(p + sbase + (size_t)pix * VB, outv);
 }
 
 // gather (prologue of the x-update, block_6_admm_loop_ver2.py:85-95,137-140):

@@ -61,6 +61,11 @@ extern "C" {
 #define ADMM_FUSE_WEIGHTED 1 /* z = (W_i a_i + W_j a_j)/(W_i + W_j)  (commented at _ver2:221-222;
                                 ADMM_Algo.pdf eq.(2)); keeps both endpoint duals */
 
+/* admm_batch.flags: x_ext's local rows are written only by admm_node_update (the caller
+ * never changes x between updates), so an update may start from the previous update's
+ * diagnostics instead of projecting x again. */
+#define ADMM_BATCH_KEEP_X 1
+
 /* per-node statistics written by admm_node_update (float64) */
 #define ADMM_NODE_STAT_MSE_SINO 0 /* ||A x - b||^2           (block_6_admm_loop_ver2.py:190-194) */
 #define ADMM_NODE_STAT_G2 1       /* ||g||^2 stationarity    (block_6_admm_loop_ver2.py:145-149) */
@@ -125,7 +130,7 @@ typedef struct admm_batch {
     /* ABI 2: edge fusion.  MIDPOINT keeps the single-y form (y_ij,max = -y);
      * WEIGHTED needs y_b and w (both NULL for MIDPOINT). */
     int32_t fusion;       /* ADMM_FUSE_* */
-    int32_t reserved2;
+    int32_t flags;        /* ADMM_BATCH_* (0 in ABI-2 callers that predate it: was reserved) */
     double* y_b;          /* [E][n] dual of the higher-numbered endpoint (y_ij,max)   */
     const double* w;      /* [n_xext][n] W of the node in each x_ext row (W_i, make_precisions) */
 } admm_batch;
