@@ -261,6 +261,8 @@ def main():
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": fwd_traffic,
             "traffic_source": TRAFFIC_FILE if fwd_traffic is not None else None,
+            # measured DRAM rate of the same launch: PMC bytes / event-timed duration
+            "traffic_gbs": fwd_traffic / (fwd_ms * 1e-3) / 1e9 if fwd_traffic is not None else None,
             "avg_launch_ms": fwd_ms,
             "bytes_per_launch": B_A * plan.V,
             "note": "sample-touch bytes (SURVEY 8d); image/sinogram are L2/MALL resident, so frac>1 "
