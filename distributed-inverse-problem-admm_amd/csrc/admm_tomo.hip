@@ -281,17 +281,21 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false) {
   hipLaunchKernelGGL((k_pack_d<T, VB>), dim3((unsigned)((npix + 255) / 256), nch), dim3(256), 0, s, B.dsum,
                      (T*)C->dsumS.p, (int)npix, V);
   CHECK_LAUNCH();
+  if (reuse) {
+    // 1-4. one kernel from the previous update's A^T (A xs - b) (ADMM_BATCH_KEEP_X):
+    //      c, r = A^T b + rho c + mu K^T(d - e) - H x, p = r (+ transpose)
+    hipLaunchKernelGGL((k_start_reuse<T, VB>), cgg, dim3(kBlock), 0, s, (const T*)C->ats.p, B.x_ext, B.y, B.z,
+                       B.q, B.inc_off, B.inc_edge, B.inc_qslot, B.inc_sign,
+                       B.fusion == ADMM_FUSE_WEIGHTED ? B.y_b : nullptr, B.atb, c, B.dsum, B.d, B.e, r, p, pT,
+                       B.rho, B.mu, N, V);
+    CHECK_LAUNCH();
+  } else {
   // 1. neighbour gather: c = sum_j q_ij (z_ij - y_ij,i); xs = (T) x (+ transpose)
   hipLaunchKernelGGL((k_gather<T, VB>), tg, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.q, B.inc_off, B.inc_edge,
                      B.inc_qslot, B.inc_sign, B.fusion == ADMM_FUSE_WEIGHTED ? B.y_b : nullptr, c, xs, xsT,
                      N, V);
   CHECK_LAUNCH();
   // 2-4. r = A^T b + rho c + mu K^T(d - e) - H x,  p = r,  rr
-  if (reuse) {  // A^T A xs from the previous update's diagnostics (ADMM_BATCH_KEEP_X)
-    hipLaunchKernelGGL((k_init_reuse<T, VB>), cgg, dim3(kBlock), 0, s, (const T*)C->ats.p, xs, B.atb, c, B.dsum,
-                       B.d, B.e, r, p, B.rho, B.mu, N, V);
-    CHECK_LAUNCH();
-  } else {
   RET((launch_fwd_batch<T, VB, 0>(C, xs, xsT, sino, nullptr, nullptr, V, s)));
   {
     BackArgs<T> a{};
@@ -309,9 +313,9 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false) {
     a.mu = B.mu;
     RET((launch_back<T, VB, BACK_INIT>(C, a, V, s)));
   }
-  }
   hipLaunchKernelGGL((k_transpose<T, VB>), tg, dim3(kBlock), 0, s, p, pT, N);
   CHECK_LAUNCH();
+  }
 
   const double tau = B.lam / B.mu;
   double* dcur = B.d;

@@ -793,7 +793,7 @@ __device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j
     gstore<T, VB>(A.out_t + sbase + (size_t)pix * VB, outv);
   } else if constexpr (MODE == BACK_DIAG) {
     // A^T s = A^T (A xs - b) of the final x: kept (out_t != null) so the next x-update
-    // can start without projecting x again (k_init_reuse)
+    // can start without projecting x again (k_start_reuse)
     if (A.out_t) gstore<T, VB>(A.out_t + sbase + (size_t)pix * VB, acc);
 #pragma unroll
     for (int u = 0; u < VB; ++u) {
@@ -1086,65 +1086,71 @@ __device__ __forceinline__ void tile_store_T(TileT<T, VB>& tl, T* __restrict__ o
 
 // CG start from the previous x-update's diagnostics (batch flag ADMM_BATCH_KEEP_X: x_ext's
 // local rows were last written by admm_node_update).  The previous DIAG left
-// ats = A^T (A xs - b) for this very xs, so A^T A xs = ats + A^T b needs no projection:
+// ats = A^T (A xs - b) for this very xs = (T) x, so A^T A xs = ats + A^T b needs no
+// projection.  One kernel replaces gather + BACK_INIT + transpose:
+//   c = sum_j q_ij (z_ij - y_ij,i)                         (k_gather's sum, same order)
 //   r = A^T b + rho c + mu K^T (d - e) - (ats + A^T b + rho D xs + mu K^T K xs),  p = r
-// (BACK_INIT's epilogue with its projected A^T A xs replaced).  One thread per pixel,
-// all VB nodes of the chunk; (kBlock / kTile) x kTile pixels per block (the CG update's grid).
+// (BACK_INIT's epilogue with its projected A^T A xs replaced; xs and its four neighbours
+// are (T) x read straight from x), p also written transposed.  One thread per pixel, all
+// VB nodes of the chunk; a block is kTile x kCgRows pixels (the CG update's grid).
 template <typename T, int VB>
-__global__ __launch_bounds__(kBlock) void k_init_reuse(const T* __restrict__ ats, const T* __restrict__ xs,
-                                                       const double* __restrict__ atb,
-                                                       const double* __restrict__ cvec,
-                                                       const double* __restrict__ dsum, const double* __restrict__ dvar,
-                                                       const double* __restrict__ evar, double* __restrict__ r,
-                                                       T* __restrict__ p, double rho, double mu, int N, int V) {
+__global__ __launch_bounds__(kBlock) void k_start_reuse(
+    const T* __restrict__ ats, const double* __restrict__ x, const double* __restrict__ y,
+    const double* __restrict__ z, const double* __restrict__ q, const int* __restrict__ inc_off,
+    const int* __restrict__ inc_edge, const int* __restrict__ inc_qslot, const int* __restrict__ inc_sign,
+    const double* __restrict__ yb, const double* __restrict__ atb, double* __restrict__ cvec,
+    const double* __restrict__ dsum, const double* __restrict__ dvar, const double* __restrict__ evar,
+    double* __restrict__ r, T* __restrict__ p, T* __restrict__ pT, double rho, double mu, int N, int V) {
+  constexpr int ROWS = kBlock / kTile;
+  __shared__ T tl[ROWS][kTile + 1][VB];
   const int chunk = blockIdx.z, v0 = chunk * VB, nv = min(VB, V - v0);
   const int npix = N * N;
   const size_t sbase = (size_t)chunk * npix * VB;
   const int jj = threadIdx.x % kTile, ii = threadIdx.x / kTile;
-  const int i = blockIdx.y * (kBlock / kTile) + ii, j = blockIdx.x * kTile + jj;
-  if (i >= N || j >= N) return;
-  const int pix = i * N + j;
-  const T* pv = xs + sbase;
-  T pc[VB], pn[VB], av[VB];
-  double ktk[VB];
-  gload<T, VB>(pv + (size_t)pix * VB, pc);
-  gload<T, VB>(ats + sbase + (size_t)pix * VB, av);
+  const int i0 = blockIdx.y * ROWS, j0 = blockIdx.x * kTile;
+  const int i = i0 + ii, j = j0 + jj;
+  if (i < N && j < N) {
+    const int pix = i * N + j;
+    T av[VB], outv[VB];
+    gload<T, VB>(ats + sbase + (size_t)pix * VB, av);
 #pragma unroll
-  for (int u = 0; u < VB; ++u) ktk[u] = 0.0;
-  if (i >= 1) {
-    gload<T, VB>(pv + (size_t)(pix - N) * VB, pn);
-#pragma unroll
-    for (int u = 0; u < VB; ++u) ktk[u] += (double)pc[u] - (double)pn[u];
-  }
-  if (i <= N - 2) {
-    gload<T, VB>(pv + (size_t)(pix + N) * VB, pn);
-#pragma unroll
-    for (int u = 0; u < VB; ++u) ktk[u] -= (double)pn[u] - (double)pc[u];
-  }
-  if (j >= 1) {
-    gload<T, VB>(pv + (size_t)(pix - 1) * VB, pn);
-#pragma unroll
-    for (int u = 0; u < VB; ++u) ktk[u] += (double)pc[u] - (double)pn[u];
-  }
-  if (j <= N - 2) {
-    gload<T, VB>(pv + (size_t)(pix + 1) * VB, pn);
-#pragma unroll
-    for (int u = 0; u < VB; ++u) ktk[u] -= (double)pn[u] - (double)pc[u];
-  }
-  T outv[VB];
-#pragma unroll
-  for (int u = 0; u < VB; ++u) {
-    outv[u] = T(0);
-    if (u < nv) {
-      const size_t vo = (size_t)(v0 + u) * npix;
-      const double ab = atb[vo + pix];
-      const double h = ((double)av[u] + ab) + rho * dsum[vo + pix] * (double)pc[u] + mu * ktk[u];
-      const double rr = ab + rho * cvec[vo + pix] + mu * kt_w_at(dvar + 2 * vo, evar + 2 * vo, N, i, j) - h;
-      r[vo + pix] = rr;
-      outv[u] = (T)rr;
+    for (int u = 0; u < VB; ++u) {
+      outv[u] = T(0);
+      if (u < nv) {
+        const int v = v0 + u;
+        const size_t vo = (size_t)v * npix;
+        const double* xv = x + vo;
+        double cc = 0.0;
+        for (int qq = inc_off[v]; qq < inc_off[v + 1]; ++qq) {
+          const size_t eo = (size_t)inc_edge[qq] * npix + pix;
+          const double vij = edge_v(z, y, yb, inc_sign[qq], eo);
+          cc += q[(size_t)inc_qslot[qq] * npix + pix] * vij;
+        }
+        cvec[vo + pix] = cc;
+        // K^T K xs at (i, j) from (T) x, in BACK_INIT's order
+        const double pcd = (double)(T)xv[pix];
+        double ktk = 0.0;
+        if (i >= 1) ktk += pcd - (double)(T)xv[pix - N];
+        if (i <= N - 2) ktk -= (double)(T)xv[pix + N] - pcd;
+        if (j >= 1) ktk += pcd - (double)(T)xv[pix - 1];
+        if (j <= N - 2) ktk -= (double)(T)xv[pix + 1] - pcd;
+        const double ab = atb[vo + pix];
+        const double h = ((double)av[u] + ab) + rho * dsum[vo + pix] * pcd + mu * ktk;
+        const double rr = ab + rho * cc + mu * kt_w_at(dvar + 2 * vo, evar + 2 * vo, N, i, j) - h;
+        r[vo + pix] = rr;
+        outv[u] = (T)rr;
+      }
+      tl[ii][jj][u] = outv[u];
     }
+    gstore<T, VB>(p + sbase + (size_t)pix * VB, outv);
   }
-  gstore<T, VB>(p + sbase + (size_t)pix * VB, outv);
+  __syncthreads();
+  // transposed copy: pT[j][i][u], runs of ROWS x VB samples per column
+  const int u = threadIdx.x % VB, rr_ = (threadIdx.x / VB) % ROWS, c0 = threadIdx.x / (VB * ROWS);
+  for (int c = c0; c < kTile; c += kBlock / (VB * ROWS)) {
+    const int jc = j0 + c, ic = i0 + rr_;
+    if (jc < N && ic < N) pT[sbase + ((size_t)jc * N + ic) * VB + u] = tl[rr_][c][u];
+  }
 }
 
 // gather (prologue of the x-update, block_6_admm_loop_ver2.py:85-95,137-140):
