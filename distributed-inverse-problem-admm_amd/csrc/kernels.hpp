@@ -791,54 +791,7 @@ __device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j
       }
     }
     gstore<T, VB>(A.out_t + sbase + (size_t)pix * VB, outv);
-  } else if constexpr (MODE == BACK_DIAG) {
-    // A^T s = A^T (A xs - b) of the final x: kept (out_t != null) so the next x-update
-    // can start without projecting x again (k_start_reuse)
-    if (A.out_t) gstore<T, VB>(A.out_t + sbase + (size_t)pix * VB, acc);
-#pragma unroll
-    for (int u = 0; u < VB; ++u) {
-      if (u >= nv) continue;
-      const int v = v0 + u;
-      const size_t vo = (size_t)v * npix;
-      const double* xv = A.x + vo;
-      const double xc = xv[pix];
-      // lam * K^T sub(Kx) at (i,j): needs the subgradient at (i,j), (i-1,j), (i,j-1)
-      double gx, gy, px, py, kts = 0.0, tvv;
-      grad_at(xv, N, i, j, gx, gy);
-      tv_sub(gx, gy, A.tv_kind, px, py);
-      tvv = (A.tv_kind == 0) ? sqrt(gx * gx + gy * gy) : fabs(gx) + fabs(gy);
-      if (i <= N - 2) kts -= px;
-      if (j <= N - 2) kts -= py;
-      if (i >= 1) {
-        double ax, ay, bx, by;
-        grad_at(xv, N, i - 1, j, ax, ay);
-        tv_sub(ax, ay, A.tv_kind, bx, by);
-        kts += bx;
-      }
-      if (j >= 1) {
-        double ax, ay, bx, by;
-        grad_at(xv, N, i, j - 1, ax, ay);
-        tv_sub(ax, ay, A.tv_kind, bx, by);
-        kts += by;
-      }
-      const double cc = A.cvec[vo + pix];
-      const double g = (double)acc[u] + A.rho * (A.dsum[vo + pix] * xc - cc) + A.lam * kts;
-      double quad = 0.0;
-      for (int q = A.inc_off[v]; q < A.inc_off[v + 1]; ++q) {
-        const size_t eo = (size_t)A.inc_edge[q] * npix + pix;
-        const double vij = edge_v(A.zv, A.yv, A.ybv, A.inc_sign[q], eo);
-        const double dd = xc - vij;
-        quad += A.qv[(size_t)A.inc_qslot[q] * npix + pix] * dd * dd;
-      }
-      pq[u][0] += g * g;
-      pq[u][1] += tvv;
-      pq[u][2] += 0.5 * A.rho * quad;
-      if (A.phantom) {
-        const double dp = xc - A.phantom[pix];
-        pq[u][3] += dp * dp;
-      }
-    }
-  }
+  }  // BACK_DIAG: diag_epilogue_tile (block-cooperative)
 }
 
 // Back projector.  Block = 64 (j) x kBTI (i) pixel tile, one pixel per thread.
@@ -881,6 +834,82 @@ constexpr int kBAngC = ADMM_BK_ANGC;  // angles per staged sinogram-window chunk
 #ifndef ADMM_BK_EXPT
 #define ADMM_BK_EXPT 0  // timing diagnostics only: 1 = no angle loop, 2 = no window loads, 3 = no H epilogue
 #endif
+// DIAG epilogue for a whole kBTJ x kBTI tile (block-cooperative; replaces the per-pixel
+// DIAG branch of back_epilogue, same formulas in the same order, so bitwise the same):
+// per node, x over the tile plus one halo row/column on each side is staged in LDS and
+// the TV subgradient of every point (tile + the halo row/column above/left) is computed
+// ONCE into LDS -- the per-pixel form evaluated it at three points and re-read x nine
+// times.  `scratch`: (kBTI+2)(kBTJ+2) + 2 (kBTI+1)(kBTJ+1) doubles of LDS.
+template <typename T, int VB>
+__device__ __forceinline__ void diag_epilogue_tile(const BackArgs<T>& A, double* scratch, int ib, int jb, int i,
+                                                   int j, bool inb, int chunk, int v0, int nv, const T (&acc)[VB],
+                                                   double (&pq)[VB][4]) {
+  constexpr int XC = kBTJ + 2, XR = kBTI + 2, SC = kBTJ + 1, SR = kBTI + 1;
+  double* xt = scratch;            // [XR][XC]: rows ib-1 .. ib+kBTI, cols jb-1 .. jb+kBTJ
+  double* sx = xt + XR * XC;       // [SR][SC]: subgradient at rows ib-1 .. ib+kBTI-1, cols jb-1 ..
+  double* sy = sx + SR * SC;
+  const int N = A.N, npix = N * N;
+  const int pix = i * N + j;
+  const size_t sbase = (size_t)chunk * npix * VB;
+  if (inb && A.out_t) gstore<T, VB>(A.out_t + sbase + (size_t)pix * VB, acc);
+  const int ti = i - ib + 1, tj = j - jb + 1;  // this pixel in the staged x tile
+#pragma unroll
+  for (int u = 0; u < VB; ++u) {  // constant bounds keep acc / pq in registers
+    if (u >= nv) break;           // block-uniform: the barriers below stay uniform
+    const int v = v0 + u;
+    const size_t vo = (size_t)v * npix;
+    const double* xv = A.x + vo;
+    __syncthreads();  // previous node's (or the tap loop's) LDS readers are done
+    for (int q = threadIdx.x; q < XR * XC; q += kBkThreads) {
+      const int rr = q / XC, cc = q % XC;
+      const int ii = ib - 1 + rr, jj = jb - 1 + cc;
+      xt[q] = (ii >= 0 && jj >= 0 && ii < N && jj < N) ? xv[ii * N + jj] : 0.0;
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < SR * SC; q += kBkThreads) {
+      const int rr = q / SC, cc = q % SC;
+      const int ii = ib - 1 + rr, jj = jb - 1 + cc;
+      double px = 0.0, py = 0.0;
+      if (ii >= 0 && jj >= 0 && ii < N && jj < N) {
+        const double c = xt[rr * XC + cc];
+        const double gx = (ii < N - 1) ? xt[(rr + 1) * XC + cc] - c : 0.0;
+        const double gy = (jj < N - 1) ? xt[rr * XC + cc + 1] - c : 0.0;
+        tv_sub(gx, gy, A.tv_kind, px, py);
+      }
+      sx[q] = px;
+      sy[q] = py;
+    }
+    __syncthreads();
+    if (!inb) continue;
+    const double xc = xt[ti * XC + tj];
+    const double gx = (i < N - 1) ? xt[(ti + 1) * XC + tj] - xc : 0.0;
+    const double gy = (j < N - 1) ? xt[ti * XC + tj + 1] - xc : 0.0;
+    const double tvv = (A.tv_kind == 0) ? sqrt(gx * gx + gy * gy) : fabs(gx) + fabs(gy);
+    // lam * K^T sub(Kx) at (i,j): subgradients at (i,j), (i-1,j), (i,j-1)
+    double kts = 0.0;
+    if (i <= N - 2) kts -= sx[ti * SC + tj];
+    if (j <= N - 2) kts -= sy[ti * SC + tj];
+    if (i >= 1) kts += sx[(ti - 1) * SC + tj];
+    if (j >= 1) kts += sy[ti * SC + tj - 1];
+    const double cc = A.cvec[vo + pix];
+    const double g = (double)acc[u] + A.rho * (A.dsum[vo + pix] * xc - cc) + A.lam * kts;
+    double quad = 0.0;
+    for (int q = A.inc_off[v]; q < A.inc_off[v + 1]; ++q) {
+      const size_t eo = (size_t)A.inc_edge[q] * npix + pix;
+      const double vij = edge_v(A.zv, A.yv, A.ybv, A.inc_sign[q], eo);
+      const double dd = xc - vij;
+      quad += A.qv[(size_t)A.inc_qslot[q] * npix + pix] * dd * dd;
+    }
+    pq[u][0] += g * g;
+    pq[u][1] += tvv;
+    pq[u][2] += 0.5 * A.rho * quad;
+    if (A.phantom) {
+      const double dp = xc - A.phantom[pix];
+      pq[u][3] += dp * dp;
+    }
+  }
+}
+
 template <typename T, int VB, int MODE>
 __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
   constexpr int NQ = (MODE == BACK_H) ? 5 : (MODE == BACK_DIAG) ? 4 : 1;
@@ -1020,7 +1049,10 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
   for (int u = 0; u < VB; ++u)
 #pragma unroll
     for (int q = 0; q < NQ; ++q) pq[u][q] = 0.0;
-  if (inb) {
+  if constexpr (MODE == BACK_DIAG) {
+    __shared__ double diag_s[(kBTI + 2) * (kBTJ + 2) + 2 * (kBTI + 1) * (kBTJ + 1)];
+    diag_epilogue_tile<T, VB>(A, diag_s, ib, jb, i, j, inb, chunk, v0, nv, acc, pq);
+  } else if (inb) {
     if constexpr (ADMM_BK_EXPT == 3 && MODE == BACK_H) {
       gstore<T, VB>(A.out_t + (size_t)chunk * N * N * VB + (size_t)(i * N + j) * VB, acc);
     } else {
