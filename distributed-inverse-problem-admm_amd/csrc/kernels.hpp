@@ -387,6 +387,9 @@ constexpr int kFgG = ADMM_FG_G;        // max angles (waves) per block
 constexpr int kFgThreads = 64 * kFgG;
 constexpr int kFgWin = ADMM_FG_WIN;    // staged window width (pixels)
 constexpr int kFgSeg = ADMM_FG_SEG;    // row segments (partial sums) per ray
+#ifndef ADMM_FG_W4
+#define ADMM_FG_W4 1  // chunk window origins as one int4 LDS read into scalars (0: one read per row)
+#endif
 #ifndef ADMM_FG_EO
 #define ADMM_FG_EO 1  // even/odd half-window LDS layout (0: plain pixel order, tuning only)
 #endif
@@ -447,8 +450,8 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
 
   __shared__ Pack<T, PV> win[NPL][kFgRows][kFgRow];
   // every row window of the segment (N <= 4096): origin and the width actually touched
-  __shared__ int wlo_s[(4096 + kFgSeg - 1) / kFgSeg];
-  __shared__ int wnum_s[(4096 + kFgSeg - 1) / kFgSeg];
+  __shared__ __align__(16) int wlo_s[(4096 + kFgSeg - 1) / kFgSeg + 4];  // +4: int4 reads of the last chunk
+  __shared__ int wnum_s[(4096 + kFgSeg - 1) / kFgSeg + 4];
   for (int r = threadIdx.x; r < nrows; r += kFgThreads) {
     const double dm = (double)(m_lo + r);
     double lmin = 1e300, lmax = -1e300;
@@ -483,7 +486,9 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       const int pl = q % NPL, rw = q / NPL;
       const int r = rw / kFgWin, w = rw - r * kFgWin;
       // only the row's touched width is fetched (the rest of the window is never read)
-      const int col = (r < rows && w < wnum_s[m0 - m_lo + r]) ? wlo_s[m0 - m_lo + r] + w : -1;
+      // both reads unconditional (in bounds: +4 padding), so they issue together
+      const int wn = wnum_s[m0 - m_lo + r], wo = wlo_s[m0 - m_lo + r];
+      const int col = (r < rows && w < wn) ? wo + w : -1;
       if (q < kFgRows * kFgWin * NPL && col >= 0 && col < N) {
         stage[e] = *reinterpret_cast<const Pack<T, PV>*>(src + ((size_t)(m0 + r) * N + col) * VB + pl * PV);
       } else {
@@ -517,6 +522,19 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   if (ADMM_FG_EXPT != 2) fetch(m_lo);
   for (int m0 = m_lo; m0 < m_hi; m0 += kFgRows) {
     const int rows = (ADMM_FG_EXPT == 1) ? 0 : min(kFgRows, m_hi - m0);
+    // the chunk's window origins, read once into scalar registers (a per-row LDS read
+    // would put a dependent LDS round trip in front of every row's tap reads)
+    int wl[kFgRows];
+    if constexpr (ADMM_FG_W4 && kFgRows == 4) {
+      const int4 w4 = *reinterpret_cast<const int4*>(&wlo_s[m0 - m_lo]);
+      wl[0] = __builtin_amdgcn_readfirstlane(w4.x);
+      wl[1] = __builtin_amdgcn_readfirstlane(w4.y);
+      wl[2] = __builtin_amdgcn_readfirstlane(w4.z);
+      wl[3] = __builtin_amdgcn_readfirstlane(w4.w);
+    } else {
+#pragma unroll
+      for (int r = 0; r < kFgRows; ++r) wl[r] = wlo_s[m0 - m_lo + r];
+    }
     __syncthreads();  // previous chunk's readers are done
     if (ADMM_FG_EXPT != 2) commit();
     __syncthreads();
@@ -527,13 +545,13 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       int idx;
       T w1;
       if constexpr (std::is_same<T, float>::value) {
-        idx = (int)(lfix >> 32) - wlo_s[m0 - m_lo + r];
+        idx = (int)(lfix >> 32) - wl[r];
         w1 = (float)(unsigned)lfix * 2.3283064365386963e-10f;  // fraction * 2^-32
         lfix += dlfix;
       } else {
         const double l = fma((double)(m0 + r), a.dl, l0);
         const double fl = floor(l);
-        idx = (int)fl - wlo_s[m0 - m_lo + r];
+        idx = (int)fl - wl[r];
         w1 = (T)(l - fl);
       }
       const T w0 = T(1) - w1;
