@@ -38,6 +38,7 @@ ANGLES_PER_NODE = 96
 LAM, RHO = 0.02, 2.0
 TV_ITERS, CG_ITERS = 10, 5
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+LDS_PEAK_GBS = 150000.0  # aggregate ds_read_b128 rate, every CU streaming (MI355X_MICROARCH.md, LDS)
 
 
 # BASELINE.json configs[1..4]: image side, total graph nodes, graph, dtype, TV
@@ -222,6 +223,7 @@ def main():
     sbytes = 8 if dtype == "float64" else 4
     B_A, B_At, B_node = node_bytes(n_img, a_node, TV_ITERS, CG_ITERS, sbytes)
     achieved = B_A * plan.V / (fwd_ms * 1e-3) / 1e9
+    lds_bytes = sbytes * a_node * n_img * 2 * n_img * plan.V  # m rays x N rows x 2 taps x V samples
     fwd_traffic = pmc_traffic(FWD_KERNELS) if not args.config else None
     if args.config:
         workload = (f"{args.config}: {n_img}^2, {V_total} graph nodes ({CONFIGS[args.config]['graph']}), "
@@ -267,6 +269,17 @@ def main():
             "bytes_per_launch": B_A * plan.V,
             "note": "sample-touch bytes (SURVEY 8d); image/sinogram are L2/MALL resident, so frac>1 "
                     "means on-chip reuse, see DESIGN.md",
+            # the bound that actually applies on chip: every tap is an LDS read of the staged
+            # window (2 taps x V samples per ray and row), against the measured ds_read_b128 peak
+            "lds": {
+                "achieved": lds_bytes / (fwd_ms * 1e-3) / 1e9,
+                "peak": LDS_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": lds_bytes / (fwd_ms * 1e-3) / 1e9 / LDS_PEAK_GBS,
+                "bytes_per_launch": lds_bytes,
+                "note": "tap reads only (staging writes excluded); peak = MI355X_MICROARCH.md aggregate "
+                        "ds_read_b128 rate, all CUs streaming",
+            },
         },
         "node_update_bytes": B_node,
         "node_update_gbs": B_node * value / world / 1e9,
