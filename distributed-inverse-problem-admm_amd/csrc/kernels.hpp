@@ -849,6 +849,9 @@ constexpr int kBWin = ((ce_isqrt_ceil((kBTJ - 1) * (kBTJ - 1) + (kBTI - 1) * (kB
 #endif
 constexpr int kBAngC = ADMM_BK_ANGC;  // angles per staged sinogram-window chunk
 
+#ifndef ADMM_BK_PF
+#define ADMM_BK_PF 1  // register-prefetched sinogram windows (0: stage each chunk after its kmin)
+#endif
 #ifndef ADMM_BK_EXPT
 #define ADMM_BK_EXPT 0  // timing diagnostics only: 1 = no angle loop, 2 = no window loads, 3 = no H epilogue
 #endif
@@ -955,7 +958,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
   // window stays at 48 KB of LDS
   constexpr int ANGC = (NPL > 2) ? kBAngC / 2 : kBAngC;
   __shared__ Pack<T, PV> win[NPL][(MODE == BACK_WSQ) ? 1 : ANGC][kBWin];
-  __shared__ int4 kmin_s[ANGC / 4];
+  __shared__ int4 kmin_s[2][ANGC / 4];
   T acc[VB];
 #pragma unroll
   for (int u = 0; u < VB; ++u) acc[u] = T(0);
@@ -1003,30 +1006,69 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
     }
   };
 
-  for (int t0 = 0; t0 < n_ang; t0 += ANGC) {
+  // sinogram windows (MODE != WSQ).  ADMM_BK_PF: the next chunk's window is fetched into
+  // registers before this chunk's taps and written to LDS after them (the single block per
+  // CU otherwise waits for every chunk's loads with nothing to overlap; +12 VGPRs, still
+  // 4 waves/SIMD); kmin is double-buffered.  Otherwise: compute kmin, stage, tap per chunk.
+  // (float samples, H/INIT modes: the float64 and DIAG variants would spill)
+  constexpr bool PF = ADMM_BK_PF && std::is_same<T, float>::value && (MODE == BACK_H || MODE == BACK_INIT ||
+                                                                     MODE == BACK_PLAIN || MODE == BACK_ATB);
+  constexpr int SPER = (ANGC * kBWin * NPL + kBkThreads - 1) / kBkThreads;
+  Pack<T, PV> wst[SPER];
+  auto kmin_chunk = [&](int t0, int buf) {
     const int nt = min(ANGC, n_ang - t0);
-    if constexpr (MODE != BACK_WSQ) {
-      __syncthreads();
-      if ((int)threadIdx.x < nt) {
-        const BackAngleC g = A.angc[t0 + threadIdx.x];
-        auto kf = [&](int ii, int jj) { return fma((double)ii - c0, g.Bi, fma((double)jj - c0, g.Bj, Kc)); };
-        const double kmn = fmin(fmin(kf(ib, jb), kf(ib, jhi)), fmin(kf(ihi, jb), kf(ihi, jhi)));
-        reinterpret_cast<int*>(kmin_s)[threadIdx.x] = (int)floor(kmn) - 1;
-      }
-      __syncthreads();
-      for (int q = threadIdx.x; q < nt * kBWin * NPL; q += kBkThreads) {
-        const int pl = q % NPL, aw = q / NPL;
-        const int a = aw / kBWin, w = aw - a * kBWin;
-        const int k = reinterpret_cast<const int*>(kmin_s)[a] + w;
-        Pack<T, PV> val;
-        if (ADMM_BK_EXPT != 2 && k >= 0 && k < n_det) {
-          val = *reinterpret_cast<const Pack<T, PV>*>(sino_c + ((size_t)(t0 + a) * n_det + k) * VB + pl * PV);
-        } else {
+    if ((int)threadIdx.x < nt) {
+      const BackAngleC g = A.angc[t0 + threadIdx.x];
+      auto kf = [&](int ii, int jj) { return fma((double)ii - c0, g.Bi, fma((double)jj - c0, g.Bj, Kc)); };
+      const double kmn = fmin(fmin(kf(ib, jb), kf(ib, jhi)), fmin(kf(ihi, jb), kf(ihi, jhi)));
+      reinterpret_cast<int*>(kmin_s[buf])[threadIdx.x] = (int)floor(kmn) - 1;
+    }
+  };
+  auto wfetch = [&](int t0, int buf) {
+    const int nt = min(ANGC, n_ang - t0);
 #pragma unroll
-          for (int e = 0; e < PV; ++e) val.v[e] = T(0);
-        }
-        win[pl][a][w] = val;
+    for (int e = 0; e < SPER; ++e) {
+      const int q = threadIdx.x + e * kBkThreads;
+      const int pl = q % NPL, aw = q / NPL;
+      const int a = aw / kBWin, w = aw - a * kBWin;
+      const int k = (a < nt) ? reinterpret_cast<const int*>(kmin_s[buf])[a] + w : -1;
+      if (ADMM_BK_EXPT != 2 && a < nt && k >= 0 && k < n_det) {
+        wst[e] = *reinterpret_cast<const Pack<T, PV>*>(sino_c + ((size_t)(t0 + a) * n_det + k) * VB + pl * PV);
+      } else {
+#pragma unroll
+        for (int z = 0; z < PV; ++z) wst[e].v[z] = T(0);
       }
+    }
+  };
+  auto wcommit = [&](int t0) {
+    const int nt = min(ANGC, n_ang - t0);
+#pragma unroll
+    for (int e = 0; e < SPER; ++e) {
+      const int q = threadIdx.x + e * kBkThreads;
+      const int pl = q % NPL, aw = q / NPL;
+      const int a = aw / kBWin, w = aw - a * kBWin;
+      if (a < nt) win[pl][a][w] = wst[e];
+    }
+  };
+  if constexpr (PF) {
+    kmin_chunk(0, 0);
+    __syncthreads();
+    wfetch(0, 0);
+    wcommit(0);
+    if (ANGC < n_ang) kmin_chunk(ANGC, 1);
+    __syncthreads();
+  }
+  for (int t0 = 0, ci = 0; t0 < n_ang; t0 += ANGC, ++ci) {
+    const int nt = min(ANGC, n_ang - t0);
+    const int kb = (PF) ? (ci & 1) : 0;  // kmin buffer of this chunk
+    if constexpr (PF) {
+      if (t0 + ANGC < n_ang) wfetch(t0 + ANGC, kb ^ 1);  // in flight during this chunk's taps
+    } else if constexpr (MODE != BACK_WSQ) {
+      __syncthreads();
+      kmin_chunk(t0, 0);
+      __syncthreads();
+      wfetch(t0, 0);
+      wcommit(t0);
       __syncthreads();
     }
     // angles in groups of 4: the group's constants are scalar-loaded together (one
@@ -1039,7 +1081,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) g[u] = A.angc[t0 + tt + u];
       int4 km = make_int4(0, 0, 0, 0);
-      if constexpr (MODE != BACK_WSQ) km = kmin_s[tt >> 2];
+      if constexpr (MODE != BACK_WSQ) km = kmin_s[kb][tt >> 2];
       const int kms[4] = {km.x, km.y, km.z, km.w};
 #pragma unroll
       for (int u = 0; u < 4; u += 2) {
@@ -1054,11 +1096,19 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
     for (; tt < nt; ++tt) {
       const BackAngleC g = A.angc[t0 + tt];
       int km = 0;
-      if constexpr (MODE != BACK_WSQ) km = reinterpret_cast<const int*>(kmin_s)[tt];
+      if constexpr (MODE != BACK_WSQ) km = reinterpret_cast<const int*>(kmin_s[kb])[tt];
       T wa0, wa1;
       Pack<T, PV> sa0[NPL], sa1[NPL];
       tap(g, km, wa0, wa1, sa0, sa1, tt);
       fmac(wa0, wa1, sa0, sa1);
+    }
+    if constexpr (PF) {
+      if (t0 + ANGC < n_ang) {
+        __syncthreads();  // this chunk's taps are done with win and kmin_s[kb]
+        wcommit(t0 + ANGC);
+        if (t0 + 2 * ANGC < n_ang) kmin_chunk(t0 + 2 * ANGC, kb);
+        __syncthreads();
+      }
     }
   }
 
