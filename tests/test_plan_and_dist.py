@@ -169,21 +169,23 @@ def run_sharded(rank, world, gname, HaloExchange, assemble_stats, gather_images,
     return X.numpy().copy(), hist
 
 
-@pytest.mark.parametrize("gname", ["ring8", "complete6", "er9"])
-def test_world2_gloo_matches_single_process_bitwise(gname):
+# world 2: both halo directions go to the same peer; world 4 on the ring: distinct left and
+# right peers (the 8-GPU layout), on the ER graph an uneven 3/2/2/2 split and the all-gather
+@pytest.mark.parametrize("gname,world", [("ring8", 2), ("complete6", 2), ("er9", 2), ("ring8", 4), ("er9", 4)])
+def test_gloo_sharded_matches_single_process_bitwise(gname, world):
     from admm_hip.exchange import HaloExchange, assemble_stats, gather_images
     X1, h1 = run_sharded(0, 1, gname, HaloExchange, assemble_stats, gather_images, make_plan)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sharded_oracle_admm, args=(r, 2, port, gname, q)) for r in range(2)]
+    procs = [ctx.Process(target=_sharded_oracle_admm, args=(r, world, port, gname, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=240) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for r in range(2):
+    for r in range(world):
         X2, h2 = res[r]
         assert np.array_equal(X1, X2), gname
         assert h1["primal"] == h2["primal"] and h1["dual"] == h2["dual"], gname
