@@ -339,7 +339,10 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false) {
       a.mu = B.mu;
       RET((launch_back<T, VB, BACK_H>(C, a, V, s)));
       RET(launch_reduce((double*)C->partH.p, 5 * V, Pb, redH, 1, 1, 0, s));
-      hipLaunchKernelGGL((k_cg_update<T, VB>), cgg, dim3(kBlock), 0, s, B.x_ext, r, p, pT, Hp, redH, N, V);
+      if (kk + 1 < K || !ADMM_CG_SKIP_P)
+        hipLaunchKernelGGL((k_cg_update<T, VB, true>), cgg, dim3(kBlock), 0, s, B.x_ext, r, p, pT, Hp, redH, N, V);
+      else  // p is overwritten next (TV update / next x-update start)
+        hipLaunchKernelGGL((k_cg_update<T, VB, false>), cgg, dim3(kBlock), 0, s, B.x_ext, r, p, pT, Hp, redH, N, V);
       CHECK_LAUNCH();
     }
     const bool last = (t + 1 == Tt);

@@ -1314,7 +1314,12 @@ __global__ __launch_bounds__(kBlock) void k_transpose(const T* __restrict__ in, 
 // runs (a node-per-lane mapping splits those into 64-B pieces across 8 arrays 2 MB apart).
 constexpr int kCgRows = kBlock / kTile;  // 8 rows x 32 columns per block
 
-template <typename T, int VB>
+#ifndef ADMM_CG_SKIP_P
+#define ADMM_CG_SKIP_P 1  // 0: every CG step writes p (A/B timing only)
+#endif
+// WRITE_P = false: the last CG step of a split-Bregman round -- the TV update (or the next
+// x-update's start) overwrites p and its transposed copy, so only x and r are written
+template <typename T, int VB, bool WRITE_P = true>
 __global__ __launch_bounds__(kBlock) void k_cg_update(double* __restrict__ x, double* __restrict__ r,
                                                       T* __restrict__ p, T* __restrict__ pT,
                                                       const T* __restrict__ Hp, const double* __restrict__ redH,
@@ -1359,10 +1364,11 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(double* __restrict__ x, do
         r[o] = rn;
         np[u] = (T)(rn + beta * pd);
       }
-      tl[ii][jj][u] = np[u];
+      if constexpr (WRITE_P) tl[ii][jj][u] = np[u];
     }
-    gstore<T, VB>(p + sbase + (size_t)pix * VB, np);
+    if constexpr (WRITE_P) gstore<T, VB>(p + sbase + (size_t)pix * VB, np);
   }
+  if constexpr (!WRITE_P) return;
   __syncthreads();
   // transposed copy: pT[j][i][u], runs of kCgRows x VB samples per column
   const int u = threadIdx.x % VB, rr_ = (threadIdx.x / VB) % kCgRows, c0 = threadIdx.x / (VB * kCgRows);
