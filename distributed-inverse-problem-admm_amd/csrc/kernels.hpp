@@ -387,6 +387,9 @@ constexpr int kFgG = ADMM_FG_G;        // max angles (waves) per block
 constexpr int kFgThreads = 64 * kFgG;
 constexpr int kFgWin = ADMM_FG_WIN;    // staged window width (pixels)
 constexpr int kFgSeg = ADMM_FG_SEG;    // row segments (partial sums) per ray
+#ifndef ADMM_FG_PRIO
+#define ADMM_FG_PRIO 1  // wave priority raised while issuing the staging loads (2: during taps; 0: off)
+#endif
 #ifndef ADMM_FG_W4
 #define ADMM_FG_W4 1  // chunk window origins as one int4 LDS read into scalars (0: one read per row)
 #endif
@@ -538,7 +541,10 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
     __syncthreads();  // previous chunk's readers are done
     if (ADMM_FG_EXPT != 2) commit();
     __syncthreads();
+    if (ADMM_FG_PRIO == 1) __builtin_amdgcn_s_setprio(1);
     if (ADMM_FG_EXPT != 2 && m0 + kFgRows < m_hi) fetch(m0 + kFgRows);
+    if (ADMM_FG_PRIO == 1) __builtin_amdgcn_s_setprio(0);
+    if (ADMM_FG_PRIO == 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int r = 0; r < kFgRows; ++r) {  // unrolled: the chunk's LDS reads can all be in flight
       if (r >= rows) break;
@@ -581,6 +587,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         }
       }
     }
+    if (ADMM_FG_PRIO == 2) __builtin_amdgcn_s_setprio(0);
   }
   if (g < G && k >= 0 && k < n_det) {
     const size_t m_rays = (size_t)n_ang * n_det;
