@@ -8,17 +8,30 @@ samples / float64 solver state.  A "step" is one outer ADMM iteration: the
 x-update of every node, the halo exchange (RCCL), the z/y edge updates and the
 residual/statistics readback the reference's stop test needs.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--strong C4|none]
     torchrun --nproc-per-node N bench.py --gpus N ...
-    python bench.py --config C2|C3|C4|C5     (BASELINE.json configs[1..4], fixed node count,
-                                               sharded over however many ranks run it)
+    python bench.py --config C2|C3|C4|C5|C5s   (BASELINE.json configs[1..4], fixed node count,
+                                                 sharded over however many ranks run it)
 
-Rank 0 prints one JSON line.  The forward projector's average launch time is
-measured live with HIP events on the stream it runs on; its algorithmic
-(sample-touch) bytes are B_A = 4 m (2N+1) per node.  The CPU
-baseline is the float64 NumPy/SciPy oracle (oracle/, a port of the reference
-algorithm; the reference's CVXPY/ODL path cannot run here) timed on a bounded
-sample of the same workload on rank 0's host cores.
+Rank 0 prints one JSON line.  Besides the weak-scaling headline, the line carries a
+strong-scaling measurement (``strong``: BASELINE configs[3], C4 = 1024^2 / 32-node
+Erdos-Renyi graph, fixed total work, sharded over the same N ranks), so one driver
+sweep over N yields both curves.
+
+Roofline (``roofline``): the dominant kernel is the forward projector's tap kernel
+k_fwdg.  Its average launch duration is measured live with HIP events on the stream it
+runs on; its HBM bytes per launch come from the committed rocprofv3 PMC passes
+(2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md) of the in-solve launches
+(TRAFFIC_FILE), so ``frac`` = PMC bytes / live duration / 8 TB/s.  ``compulsory_bytes``
+is what one launch must move at least (each node image read once, its sinogram written
+once); ``sample_touch`` is SURVEY.md 8d's per-tap accounting, which counts LDS-served
+taps and so exceeds any memory peak -- it is reported as a reuse factor, not a rate.
+``step_hbm`` is the whole step's PMC traffic over the measured step time.
+
+CPU baseline (``cpu_baseline``): the float64 NumPy/SciPy oracle (oracle/, the port of
+the reference algorithm -- the reference's CVXPY/ODL path cannot run here) doing the
+SAME first x-update of node 0 (the GPU's own float32 sinogram, precisions and zero
+start) in one process per host core; ``rel_fro`` = GPU node-0 image vs that oracle image.
 """
 from __future__ import annotations
 
@@ -39,6 +52,7 @@ LAM, RHO = 0.02, 2.0
 TV_ITERS, CG_ITERS = 10, 5
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 LDS_PEAK_GBS = 150000.0  # aggregate ds_read_b128 rate, every CU streaming (MI355X_MICROARCH.md, LDS)
+CPU_BASELINE_SECONDS = 8.0  # per-process compute budget of the bounded CPU sample
 
 
 # BASELINE.json configs[1..4]: image side, total graph nodes, graph, dtype, TV
@@ -70,8 +84,8 @@ def make_graph(kind, V):
         seed += 1
 
 
-def node_bytes(N, a, tv, cg, sample_bytes=4):
-    """Algorithmic sample-touch bytes of one x-update (4-byte samples, 8 in C5)."""
+def sample_touch_bytes(N, a, tv, cg, sample_bytes=4):
+    """SURVEY.md 8d sample-touch bytes: (B_A, B_At, B_node) per node (4-byte samples, 8 in C5)."""
     m = a * N
     n = N * N
     sb = sample_bytes
@@ -81,93 +95,112 @@ def node_bytes(N, a, tv, cg, sample_bytes=4):
     return B_A, B_At, tv * (cg * B_cg + 27 * sb * n) + B_At + sb * n * (3 * 2 + 2)
 
 
-def cpu_baseline(seconds_budget=20.0):
-    """Oracle (float64 NumPy/SciPy) x-updates at the bench size on this host."""
+# ---------------------------------------------------------------------------
+# CPU baseline: the oracle's x-update, one spawned process per host core
+# ---------------------------------------------------------------------------
+def _cpu_worker(wid, N, a, b, q, budget, barrier, out):
+    """One process: build the Joseph CSR matrix, wait for the others, run x-updates of
+    node 0's first ADMM iteration (zero start, v = 0) until ``budget`` seconds pass."""
     import numpy as np
     from oracle import node_solver as ons
-    from oracle.geometry import Geometry, joseph_matrix, shepp_logan
-    t0 = time.perf_counter()
-    A = joseph_matrix(Geometry(N_IMG, ANGLES_PER_NODE))
+    from oracle.geometry import Geometry, joseph_matrix
+    A = joseph_matrix(Geometry(N, a))
     AT = A.T.tocsr()
-    build_s = time.perf_counter() - t0
-    x_true = shepp_logan(N_IMG, 2).ravel()
-    b = A @ x_true + 0.005 * np.random.default_rng(1000).standard_normal(A.shape[0])
-    W = np.maximum(np.asarray(A.multiply(A).sum(axis=0)).ravel(), 1e-12)
-    q = W  # arithmetic mean of identical W
+    b = np.asarray(b, dtype=np.float64)
+    q = np.asarray(q, dtype=np.float64)
     Atb = AT @ b
-    prm = ons.NodeParams(rho=RHO, lam=LAM, mu=10 * LAM, tv_iters=TV_ITERS, cg_iters=CG_ITERS)
-    n = N_IMG * N_IMG
-    st = ons.NodeState.zeros(n)
+    n = N * N
     v = np.zeros(n)
-    done = 0
+    prm = ons.NodeParams(rho=RHO, lam=LAM, mu=10 * LAM, tv_iters=TV_ITERS, cg_iters=CG_ITERS)
+    barrier.wait()
     t0 = time.perf_counter()
+    done, x = 0, None
     while True:
-        ons.node_update(A, Atb, b, 2 * q, 2 * q * v, [(q, v), (q, v)], st, N_IMG, prm, AT=AT)
+        st = ons.NodeState.zeros(n)
+        ons.node_update(A, Atb, b, 2 * q, 2 * q * v, [(q, v), (q, v)], st, N, prm, AT=AT)
         done += 1
         el = time.perf_counter() - t0
-        if el > seconds_budget or done >= 3:
+        if x is None:
+            x = st.x
+        if el >= budget:
             break
-    return {"value": done / el, "unit": "node-updates/s", "cores": 1, "kind": "port",
-            "sample": f"{done} x-update(s) of one 512^2 node (96 angles, 2 ring neighbours, "
-                      f"10x5 inner), float64 SciPy CSR Joseph matrix, single thread; "
-                      f"{el:.1f} s timed, {build_s:.1f} s matrix build excluded"}
+    out.put((wid, done, el, x if wid == 0 else None))
 
 
-# HBM bytes per forward-projector launch from the committed rocprofv3 PMC summary
-# (scripts/pmc.sh + scripts/traffic_summary.py; 2 x FETCH_SIZE + WRITE_SIZE per the
-# MI355X_MICROARCH.md gfx950 correction).  PMC counters cannot be read inside this run.
-TRAFFIC_FILE = "profiles/r1_traffic.json"
-FWD_KERNELS = ("admm::k_fwdg<float, 8>",)
+def cpu_baseline(N, a, b, q, x_gpu, procs=None, budget=CPU_BASELINE_SECONDS):
+    """Oracle x-updates of node 0 on ``procs`` host processes (one per core, 1 thread each).
 
-
-def pmc_traffic(names):
+    value = updates completed by all processes / the slowest process's compute time
+    (matrix builds excluded); rel_fro = ||x_gpu - x_oracle|| / ||x_oracle||."""
+    import multiprocessing as mp
+    import numpy as np
+    if procs is None:
+        cap = int(os.environ.get("ADMM_CPU_BASELINE_PROCS", os.environ.get("OMP_NUM_THREADS", "0")) or 0)
+        procs = os.cpu_count() or 1
+        if cap > 0:
+            procs = min(procs, cap)
+    ctx = mp.get_context("spawn")  # fresh interpreters: nothing of this process's GPU state
+    saved = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
+    for k in saved:
+        os.environ[k] = "1"
     try:
-        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), TRAFFIC_FILE)) as f:
-            k = json.load(f)["kernels"]
-        return float(sum(k[n]["hbm_bytes_per_launch"] for n in names))
-    except (OSError, KeyError, ValueError):
+        barrier = ctx.Barrier(procs)
+        out = ctx.Queue()
+        ps = [ctx.Process(target=_cpu_worker, args=(w, N, a, b, q, budget, barrier, out)) for w in range(procs)]
+        t0 = time.perf_counter()
+        for p in ps:
+            p.start()
+        res = [out.get() for _ in ps]
+        for p in ps:
+            p.join()
+        wall = time.perf_counter() - t0
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    done = sum(r[1] for r in res)
+    el = max(r[2] for r in res)
+    x_cpu = next(r[3] for r in res if r[0] == 0)
+    rel = float(np.linalg.norm(x_gpu - x_cpu) / np.linalg.norm(x_cpu))
+    return {"value": done / el, "unit": "node-updates/s", "cores": procs, "kind": "port",
+            "rel_fro": rel,
+            "sample": f"{done} x-updates of node 0's first ADMM iteration ({N}^2, {a} angles, 2 ring "
+                      f"neighbours, 10x5 inner, zero start) on the GPU run's own float32 sinogram "
+                      f"and precisions; float64 SciPy CSR Joseph oracle, {procs} processes x 1 "
+                      f"thread, {el:.1f} s of compute (CSR builds excluded; {wall:.1f} s wall); "
+                      f"rel_fro = GPU node-0 image vs the oracle image"}
+
+
+# ---------------------------------------------------------------------------
+# PMC traffic (committed rocprofv3 passes)
+# ---------------------------------------------------------------------------
+# HBM bytes per forward-projector launch and per step from the committed rocprofv3 PMC
+# summary (scripts/pmc.sh + scripts/traffic_summary.py over the launches between the
+# bench's markers, i.e. the timed steps; 2 x FETCH_SIZE + WRITE_SIZE per the
+# MI355X_MICROARCH.md gfx950 correction).  PMC counters cannot be read inside this run.
+TRAFFIC_FILE = "profiles/r2_traffic.json"
+FWD_KERNEL = "admm::k_fwdg<float, 8>"
+
+
+def pmc_traffic():
+    try:
+        with open(os.path.join(ROOT, TRAFFIC_FILE)) as f:
+            return json.load(f)
+    except (OSError, ValueError):
         return None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--fwd-reps", type=int, default=20)
-    ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
-                    help="run a BASELINE.json config (fixed node count) instead of the default workload")
-    args = ap.parse_args()
-
+def setup_run(cfg_name, world, rank, local_rank):
+    """Operators, sinograms, precisions and the bound node batch of one workload."""
     import networkx as nx
-    import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    # one process per GPU; ADMM_DIST_BACKEND=gloo (+ more ranks than GPUs) is a 1-GPU
-    # rehearsal of the sharded path only -- the measured configuration is nccl (RCCL)
-    backend = os.environ.get("ADMM_DIST_BACKEND", "nccl")
-    local_rank = local_rank % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        else:
-            dist.init_process_group(backend)
-
     from admm_hip.data import make_precisions, make_sinograms, shepp_logan
-    from admm_hip.exchange import HaloExchange, assemble_stats
+    from admm_hip.exchange import HaloExchange
     from admm_hip.plan import make_plan
     from admm_hip.solver import NodeBatch, make_operators
-
-    if args.config:
-        cfg = CONFIGS[args.config]
+    if cfg_name:
+        cfg = CONFIGS[cfg_name]
         n_img, V_total, dtype, tv_kind = cfg["N"], cfg["nodes"], cfg["dtype"], cfg["tv"]
         G = make_graph(cfg["graph"], V_total)
         angles_total = max(180, 3 * n_img)  # block_2_load_odl_data.py:31-38
@@ -188,51 +221,164 @@ def main():
     nb = NodeBatch(geom, dtype, plan, sinos, Q, RHO, LAM, 10 * LAM, TV_ITERS, CG_ITERS, tv_kind,
                    ph, local_rank, keep_x=True)
     halo = HaloExchange(plan, nb.x_ext)
-    if world > 1:
-        dist.barrier()
+    return dict(n_img=n_img, V_total=V_total, dtype=dtype, tv_kind=tv_kind, geom=geom, plan=plan,
+                nb=nb, halo=halo, Wi=Wi)
 
-    def step():
+
+def timed_steps(r, steps, warmup, world, prime=None):
+    """Warmup + K timed outer iterations (barrier + synchronize on both sides, max over
+    ranks).  ``prime(nb)`` runs right after the first x-update (before its exchange)."""
+    import torch
+    import torch.distributed as dist
+    from admm_hip.exchange import assemble_stats
+    nb, halo, plan = r["nb"], r["halo"], r["plan"]
+
+    def step(first=False):
         nb.node_update()
+        if first and prime is not None:
+            prime(nb)
         halo.run()
         nb.consensus()
         return assemble_stats(plan, nb.node_stats, nb.edge_stats[: len(plan.stored_edges)])
 
-    for _ in range(args.warmup):
+    step(first=True)  # the first (full-projection) x-update; later ones replay the reuse graph
+    for _ in range(max(0, warmup - 1)):
         step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    marks = os.environ.get("ADMM_BENCH_MARKERS") == "1"
+    if marks:
+        nb.marker()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ns, es = step()
+    for _ in range(steps):
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    if marks:
+        nb.marker()
+        torch.cuda.synchronize()
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    value = V_total * args.steps / el
+    return el
 
-    # live measurement of the dominant kernel (forward projector) on its stream
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fwd-reps", type=int, default=20)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
+                    help="run a BASELINE.json config (fixed node count) instead of the default workload")
+    ap.add_argument("--strong", default="C4",
+                    help="strong-scaling config measured after the headline ('none' to skip)")
+    ap.add_argument("--strong-steps", type=int, default=3)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    # one process per GPU; ADMM_DIST_BACKEND=gloo (+ more ranks than GPUs) is a 1-GPU
+    # rehearsal of the sharded path only -- the measured configuration is nccl (RCCL)
+    backend = os.environ.get("ADMM_DIST_BACKEND", "nccl")
+    local_rank = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
+
+    r = setup_run(args.config, world, rank, local_rank)
+    if world > 1:
+        dist.barrier()
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and not args.config
+    first = {}
+
+    def prime(nb):  # node 0's first x-update and its inputs, for the CPU parity check
+        if want_cpu:
+            first["x"] = nb.x_local[0].to("cpu").numpy().copy()
+            first["b"] = nb.b[0].to("cpu").double().numpy().copy()
+
+    el = timed_steps(r, args.steps, args.warmup, world, prime)
+    nb, plan, geom = r["nb"], r["plan"], r["geom"]
+    n_img, V_total, dtype = r["n_img"], r["V_total"], r["dtype"]
+    value = V_total * args.steps / el
+    ms_per_step = 1e3 * el / args.steps
+
+    # live measurement of the dominant kernel (forward projector taps) on its stream
     fwd_ms = nb.time_forward(args.fwd_reps)
     a_node = geom.n_angles
     sbytes = 8 if dtype == "float64" else 4
-    B_A, B_At, B_node = node_bytes(n_img, a_node, TV_ITERS, CG_ITERS, sbytes)
-    achieved = B_A * plan.V / (fwd_ms * 1e-3) / 1e9
-    lds_bytes = sbytes * a_node * n_img * 2 * n_img * plan.V  # m rays x N rows x 2 taps x V samples
-    fwd_traffic = pmc_traffic(FWD_KERNELS) if not args.config else None
+    B_A, B_At, B_node = sample_touch_bytes(n_img, a_node, TV_ITERS, CG_ITERS, sbytes)
+    V = plan.V
+    n, m = n_img * n_img, a_node * n_img
+    compulsory = V * n * sbytes + V * m * sbytes  # each node image read once, its sinogram written once
+    as_designed = 2 * V * n * sbytes + 8 * V * m * sbytes  # image + transposed copy, 8 segment partials
+    lds_bytes = sbytes * a_node * n_img * 2 * n_img * V  # m rays x N rows x 2 taps x V samples
+    tr = pmc_traffic() if not args.config and world == 1 else None
+    fwd_traffic = tr["kernels"].get(FWD_KERNEL, {}).get("hbm_bytes_per_launch") if tr else None
     if args.config:
         workload = (f"{args.config}: {n_img}^2, {V_total} graph nodes ({CONFIGS[args.config]['graph']}), "
-                    f"{a_node} angles/node, {dtype} samples, {tv_kind} TV, lam=0.02 rho=2, split-Bregman "
-                    f"{TV_ITERS}x{CG_ITERS} CG, one step = one outer ADMM iteration")
+                    f"{a_node} angles/node, {dtype} samples, {r['tv_kind']} TV, lam=0.02 rho=2, "
+                    f"split-Bregman {TV_ITERS}x{CG_ITERS} CG, one step = one outer ADMM iteration")
     else:
         workload = (f"512^2, {NODES_PER_GPU} graph nodes/GPU x {ANGLES_PER_NODE} angles (ring of "
                     f"{V_total}; N=2 == BASELINE configs[2]), lam=0.02 rho=2, split-Bregman "
                     f"{TV_ITERS}x{CG_ITERS} CG, one step = one outer ADMM iteration")
+    fwd_s = fwd_ms * 1e-3
+    roof = {
+        "kernel": f"k_fwdg<{'double' if dtype == 'float64' else 'float'},{nb.ctx_vb}> (Joseph forward "
+                  "projector taps, angle-grouped, 8 row-segment partial sums per ray)",
+        "bound": "hbm",
+        "achieved": fwd_traffic / fwd_s / 1e9 if fwd_traffic is not None else None,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": fwd_traffic / fwd_s / 1e9 / HBM_PEAK_GBS if fwd_traffic is not None else None,
+        "traffic": fwd_traffic,
+        "traffic_source": (f"{TRAFFIC_FILE}: rocprofv3 PMC 2 x FETCH_SIZE + WRITE_SIZE per in-solve "
+                           "launch (Infinity-Cache hits included)") if fwd_traffic is not None else None,
+        "avg_launch_ms": fwd_ms,
+        "compulsory_bytes": compulsory,
+        "compulsory_frac": compulsory / fwd_s / 1e9 / HBM_PEAK_GBS,
+        "as_designed_bytes": as_designed,
+        "traffic_over_compulsory": fwd_traffic / compulsory if fwd_traffic is not None else None,
+        "sample_touch_bytes": B_A * V,
+        "reuse_factor": B_A * V / compulsory,
+        "note": "frac = PMC bytes per launch / live event-timed duration / 8 TB/s. compulsory = each "
+                "node image read once + its sinogram written once; as_designed adds the transposed "
+                "image copy (case-A angles) and the 8 segment partials. sample_touch (SURVEY 8d) "
+                "counts every tap as a 4-byte load; taps are LDS reads, so it is a reuse factor, "
+                "not an HBM rate (see DESIGN.md)",
+        # the bound that actually applies on chip: every tap is an LDS read of the staged
+        # window (2 taps x V samples per ray and row), against the measured ds_read_b128 peak
+        "lds": {
+            "achieved": lds_bytes / fwd_s / 1e9,
+            "peak": LDS_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": lds_bytes / fwd_s / 1e9 / LDS_PEAK_GBS,
+            "bytes_per_launch": lds_bytes,
+            "note": "tap reads only (staging writes excluded); peak = MI355X_MICROARCH.md aggregate "
+                    "ds_read_b128 rate, all CUs streaming",
+        },
+    }
+    if roof["frac"] is not None:
+        assert roof["frac"] <= 1.0, roof
     result = {
         "metric": "ADMM node-updates/sec (whole node), 512² phantom; rel-Fro vs CPU ref",
         "value": value,
@@ -240,7 +386,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": 1e3 * el / args.steps,
+        "ms_per_step": ms_per_step,
         "higher_is_better": True,
         "scaling": "strong" if args.config else "weak",
         "vs_baseline": None,
@@ -252,41 +398,32 @@ def main():
             "graph": CONFIGS[args.config]["graph"] if args.config else "ring",
             "parallelism": f"graph-node shards x{world}",
         },
-        "roofline": {
-            "kernel": f"k_fwdg<{'double' if dtype == 'float64' else 'float'},{nb.ctx_vb}> (Joseph forward "
-                      "projector taps, angle-grouped; its 8-segment partial sums are added by "
-                      "k_fwd_combine, ~5 us at 512^2, not included)",
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": fwd_traffic,
-            "traffic_source": TRAFFIC_FILE if fwd_traffic is not None else None,
-            # measured DRAM rate of the same launch: PMC bytes / event-timed duration
-            "traffic_gbs": fwd_traffic / (fwd_ms * 1e-3) / 1e9 if fwd_traffic is not None else None,
-            "avg_launch_ms": fwd_ms,
-            "bytes_per_launch": B_A * plan.V,
-            "note": "sample-touch bytes (SURVEY 8d); image/sinogram are L2/MALL resident, so frac>1 "
-                    "means on-chip reuse, see DESIGN.md",
-            # the bound that actually applies on chip: every tap is an LDS read of the staged
-            # window (2 taps x V samples per ray and row), against the measured ds_read_b128 peak
-            "lds": {
-                "achieved": lds_bytes / (fwd_ms * 1e-3) / 1e9,
-                "peak": LDS_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": lds_bytes / (fwd_ms * 1e-3) / 1e9 / LDS_PEAK_GBS,
-                "bytes_per_launch": lds_bytes,
-                "note": "tap reads only (staging writes excluded); peak = MI355X_MICROARCH.md aggregate "
-                        "ds_read_b128 rate, all CUs streaming",
-            },
-        },
-        "node_update_bytes": B_node,
-        "node_update_gbs": B_node * value / world / 1e9,
+        "roofline": roof,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.config:
-        result["cpu_baseline"] = cpu_baseline()
-        result["cpu_baseline"]["cores"] = 1
+    if tr and tr.get("per_step") and not args.config and world == 1:
+        sb = float(tr["per_step"]["hbm_bytes"])
+        gbs = sb / (ms_per_step * 1e-3) / 1e9
+        assert gbs <= HBM_PEAK_GBS, (sb, ms_per_step)
+        result["step_hbm"] = {"bytes": sb, "achieved_gbs": gbs, "frac": gbs / HBM_PEAK_GBS,
+                              "source": f"{TRAFFIC_FILE} per_step (PMC, timed steps between markers)"}
+    if want_cpu and "x" in first:
+        result["cpu_baseline"] = cpu_baseline(n_img, a_node, first["b"], r["Wi"][0], first["x"])
+    # strong scaling: a fixed BASELINE config sharded over the same ranks
+    if args.strong and args.strong.lower() != "none" and not args.config:
+        del r, nb
+        torch.cuda.empty_cache()
+        rs = setup_run(args.strong, world, rank, local_rank)
+        if world > 1:
+            dist.barrier()
+        els = timed_steps(rs, args.strong_steps, 1, world)
+        result["strong"] = {
+            "config": args.strong, "scaling": "strong",
+            "workload": f"{rs['n_img']}^2, {rs['V_total']} graph nodes ({CONFIGS[args.strong]['graph']}), "
+                        f"{rs['geom'].n_angles} angles/node, {rs['dtype']} samples, fixed total work "
+                        f"sharded over {world} rank(s)",
+            "value": rs["V_total"] * args.strong_steps / els, "unit": "node-updates/s",
+            "ms_per_step": 1e3 * els / args.strong_steps, "steps": args.strong_steps, "warmup": 1,
+        }
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

@@ -3,7 +3,7 @@
 * ``shepp_logan``   -- modified Shepp-Logan on [-1,1]^2 (the benchmark phantom of
   SURVEY.md 8d; the reference itself uses randIm/ConstIm, Gen_Sino_Partitioned.py:5-122).
 * ``make_sinograms`` -- b_i = A_i x + sigma * N(0,1)
-  (block_2_load_odl_data.py:165-172), noise from a seeded on-device generator
+  (block_2_load_odl_data.py:148-153), noise from a seeded on-device generator
   (seed base 1000 + i; the reference is unseeded).
 * ``make_precisions`` -- W_i[p] = max(||A_i[:,p]||^2, 1e-12) and the arithmetic /
   harmonic Q_ij provider of block_3_graph_and_precisions.py:11-43, with W from

@@ -1,7 +1,7 @@
 """Parallel-beam geometry and the matrix-free ray transform (product path).
 
 ``RayTransform`` is the drop-in for one entry of the reference's
-``A_dense_list`` (block_2_load_odl_data.py:86-114 materialises ODL's
+``A_dense_list`` (block_2_load_odl_data.py:68-96 materialises ODL's
 RayTransform as a dense (m x n) float32 matrix).  The reference's hot loop uses
 that matrix only through ``A.shape[1]``, ``A @ x`` and ``A.T @ r``
 (block_6_admm_loop_ver2.py:26,145,193) and column norms
@@ -23,7 +23,7 @@ from . import _lib
 
 @dataclass(frozen=True)
 class ParallelBeamGeometry:
-    """ODL Parallel2dGeometry of block_2_load_odl_data.py:34-83.
+    """ODL Parallel2dGeometry of block_2_load_odl_data.py:16-65.
 
     space ``uniform_discr([-1,-1], [1,1], [N,N])``; angles
     ``uniform_partition(angle_min, angle_max, n_angles)`` midpoints;
@@ -38,7 +38,7 @@ class ParallelBeamGeometry:
 
     @property
     def n_det(self) -> int:
-        return self.N  # det_pixels = N (block_2_load_odl_data.py:62)
+        return self.N  # det_pixels = N (block_2_load_odl_data.py:44)
 
     @property
     def n(self) -> int:
@@ -55,7 +55,7 @@ class ParallelBeamGeometry:
 
 
 def split_angles(angles_total: int, num_nodes: int) -> list[int]:
-    """block_2_load_odl_data.py:53-56."""
+    """block_2_load_odl_data.py:35-38."""
     per = [angles_total // num_nodes] * num_nodes
     for i in range(angles_total % num_nodes):
         per[i] += 1

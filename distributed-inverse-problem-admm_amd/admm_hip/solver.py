@@ -163,6 +163,16 @@ class NodeBatch:
         if self.plan.stored_edges:
             _lib.check(self.lib.admm_consensus(self.ctx.h, C.c_void_p(self._s())), "admm_consensus")
 
+    def marker(self) -> None:
+        """One k_tv_grad launch (never part of an x-update or consensus): delimits the
+        bench's timed steps in rocprofv3 PMC traces (scripts/traffic_summary.py)."""
+        if getattr(self, "_mk", None) is None:
+            self._mk = torch.empty((2, self.geom.n), dtype=torch.float64, device=self.dev)
+        _lib.check(self.lib.admm_tv_grad(self.ctx.h, C.c_void_p(self.x_ext.data_ptr()),
+                                         C.c_void_p(self._mk[0].data_ptr()),
+                                         C.c_void_p(self._mk[1].data_ptr()), 1, C.c_void_p(self._s())),
+                   "admm_tv_grad")
+
     def time_forward(self, reps: int = 20) -> float:
         ms = C.c_double()
         _lib.check(self.lib.admm_time_forward(self.ctx.h, reps, C.c_void_p(self._s()), C.byref(ms)),
@@ -172,7 +182,7 @@ class NodeBatch:
 
 def make_operators(N: int, num_nodes: int, angles_total: int | None = None, dtype: str = "float32",
                    device: int = 0, det_width_factor: float = 1.0) -> list[RayTransform]:
-    """Per-node ray transforms of block_2_load_odl_data.py:34-83 (all nodes span [0, pi))."""
+    """Per-node ray transforms of block_2_load_odl_data.py:16-65 (all nodes span [0, pi))."""
     from .geometry import split_angles
     if angles_total is None:
         angles_total = max(180, 3 * N)

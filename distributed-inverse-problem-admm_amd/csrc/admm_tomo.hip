@@ -85,8 +85,11 @@ struct admm_ctx {
   int fg_nblk = 0, fg_order_nch = 0;
   hipStream_t cap = nullptr;  // private capture stream
 
-  // operator-API scratch
-  Buf op_img, op_imgT;
+  // operator-API scratch (admm_project_fwd runs the hot grouped kernel on up to 8 images
+  // per launch: node-major images packed into the interleaved sample layout)
+  Buf op_img, op_imgT, op_sino, op_fpart;
+  Buf op_order[2];  // block tables of the two forward plans for one node chunk
+  int op_nblk[2] = {0, 0};
 
   // batch
   bool bound = false;
@@ -108,6 +111,12 @@ struct admm_ctx {
 
 namespace {
 
+#define RET(expr)                   \
+  do {                              \
+    int _rc = (expr);               \
+    if (_rc != ADMM_OK) return _rc; \
+  } while (0)
+
 int vb_for(int V) { return V >= 5 ? 8 : (V >= 3 ? 4 : (V == 2 ? 2 : 1)); }
 
 void select_fwd_plan(admm_ctx* C, int pl) {
@@ -121,7 +130,7 @@ void select_fwd_plan(admm_ctx* C, int pl) {
 // first.  When every block is resident at once (<= 2 per CU) the second half is reversed so
 // the blocks sharing a CU pair heavy with light (dispatch fills one slot per CU, then the
 // second); otherwise heaviest-first is the longest-processing-time order.
-int build_fwd_order(admm_ctx* C, int pl, int nch, int cus) {
+int build_fwd_order_into(admm_ctx* C, int pl, int nch, int cus, Buf& buf, int* nblk) {
   struct Blk {
     int4 b;
     int w;
@@ -139,10 +148,15 @@ int build_fwd_order(admm_ctx* C, int pl, int nch, int cus) {
   }
   std::vector<int4> t(n);
   for (int i = 0; i < n; ++i) t[i] = v[i].b;
-  const int rc = ensure(C->fg_order, (size_t)n * sizeof(int4));
+  const int rc = ensure(buf, (size_t)n * sizeof(int4));
   if (rc != ADMM_OK) return rc;
-  HIPCHK(hipMemcpy(C->fg_order.p, t.data(), (size_t)n * sizeof(int4), hipMemcpyHostToDevice));
-  C->fg_nblk = n;
+  HIPCHK(hipMemcpy(buf.p, t.data(), (size_t)n * sizeof(int4), hipMemcpyHostToDevice));
+  *nblk = n;
+  return ADMM_OK;
+}
+
+int build_fwd_order(admm_ctx* C, int pl, int nch, int cus) {
+  RET(build_fwd_order_into(C, pl, nch, cus, C->fg_order, &C->fg_nblk));
   C->fg_order_nch = nch;
   return ADMM_OK;
 }
@@ -153,25 +167,34 @@ int build_fwd_order(admm_ctx* C, int pl, int nch, int cus) {
 // put 3 on some; co-resident blocks share the CU).  ADMM_FWD_PLAN=0/1 forces a plan.
 // (The occupancy query only guards against a plan that cannot be resident at all.)
 template <typename T, int VB>
-int choose_fwd_plan(admm_ctx* C, int V) {
-  if (C->plan_n[0] == 0) return ADMM_OK;
+int pick_fwd_plan(admm_ctx* C, int nch, int* pl_out, int* cus_out) {
   int per_cu = 0, cus = 0;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fwdg<T, VB>, kFgThreads, 0));
   HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, C->device));
   if (per_cu < 1) return fail(ADMM_E_HIP, "grouped forward projector cannot be resident");
-  const long nch = (V + VB - 1) / VB;
   auto per_cu_max = [&](int pl) { return ((long)C->plan_blocks[pl] * nch + cus - 1) / std::max(1, cus); };
   int pl = per_cu_max(1) <= per_cu_max(0) ? 1 : 0;
   const char* f = getenv("ADMM_FWD_PLAN");
   if (f && (f[0] == '0' || f[0] == '1')) pl = f[0] - '0';
   if (getenv("ADMM_DEBUG_PLAN"))
     fprintf(stderr, "[admm] forward plans: unaligned %d groups %d blocks, aligned %d groups %d blocks, "
-                    "x%ld chunks, %d CUs -> %s\n", C->plan_n[0], C->plan_blocks[0], C->plan_n[1],
+                    "x%d chunks, %d CUs -> %s\n", C->plan_n[0], C->plan_blocks[0], C->plan_n[1],
             C->plan_blocks[1], nch, cus, pl ? "aligned" : "unaligned");
+  *pl_out = pl;
+  *cus_out = cus;
+  return ADMM_OK;
+}
+
+template <typename T, int VB>
+int choose_fwd_plan(admm_ctx* C, int V) {
+  if (C->plan_n[0] == 0) return ADMM_OK;
+  const int nch = (V + VB - 1) / VB;
+  int pl = 0, cus = 0;
+  RET((pick_fwd_plan<T, VB>(C, nch, &pl, &cus)));
   select_fwd_plan(C, pl);
   return getenv("ADMM_FWD_NATURAL_ORDER") && getenv("ADMM_FWD_NATURAL_ORDER")[0] == '1'
-             ? build_fwd_order(C, pl, (int)nch, 0)
-             : build_fwd_order(C, pl, (int)nch, cus);
+             ? build_fwd_order(C, pl, nch, 0)
+             : build_fwd_order(C, pl, nch, cus);
 }
 
 template <typename F>
@@ -183,12 +206,6 @@ int with_vb(int vb, F&& f) {
     default: return f(std::integral_constant<int, 1>{});
   }
 }
-
-#define RET(expr)                   \
-  do {                              \
-    int _rc = (expr);               \
-    if (_rc != ADMM_OK) return _rc; \
-  } while (0)
 
 template <typename T, int VB, int MODE>
 int launch_fwd(admm_ctx* C, const T* img, const T* imgT, T* sino, const T* b, double* part, int V, hipStream_t s) {
@@ -202,13 +219,20 @@ int launch_fwd(admm_ctx* C, const T* img, const T* imgT, T* sino, const T* b, do
 // hot-path forward projection of the bound batch: grouped kernel + fixed-order combine
 // the grouped forward projector's tap kernel (all sample taps; segment partials -> fpart)
 template <typename T, int VB>
+int launch_fwdg_taps_with(admm_ctx* C, const T* img, const T* imgT, T* fpart, const FgGroup* groups,
+                          const int4* order, int nblk, int V, hipStream_t s) {
+  hipLaunchKernelGGL((k_fwdg<T, VB>), dim3(nblk), dim3(kFgThreads), 0, s, img, imgT, fpart, C->fang, groups, order,
+                     C->g.N, C->g.n_det, C->g.n_angles, V);
+  CHECK_LAUNCH();
+  return ADMM_OK;
+}
+
+template <typename T, int VB>
 int launch_fwdg_taps(admm_ctx* C, const T* img, const T* imgT, int V, hipStream_t s) {
   const int nch = (V + VB - 1) / VB;
   if (nch != C->fg_order_nch) return fail(ADMM_E_STATE, "forward block table built for another batch size");
-  hipLaunchKernelGGL((k_fwdg<T, VB>), dim3(C->fg_nblk), dim3(kFgThreads), 0, s, img, imgT, (T*)C->fpart.p, C->fang,
-                     C->groups, (const int4*)C->fg_order.p, C->g.N, C->g.n_det, C->g.n_angles, V);
-  CHECK_LAUNCH();
-  return ADMM_OK;
+  return launch_fwdg_taps_with<T, VB>(C, img, imgT, (T*)C->fpart.p, C->groups, (const int4*)C->fg_order.p,
+                                      C->fg_nblk, V, s);
 }
 
 template <typename T, int VB, int MODE>
@@ -445,6 +469,60 @@ int capture(admm_ctx* C, F&& fn, hipGraph_t* g, hipGraphExec_t* x) {
   return ADMM_OK;
 }
 
+// Operator API forward projection (A @ x of node-major images).  When the geometry has
+// angle-group plans this is the hot path's own kernel pair (k_fwdg + k_fwd_combine) on
+// up to 8 images per launch: the images are packed into the interleaved sample layout
+// (plus the transposed copy case-A angles read), projected, and the interleaved
+// sinograms unpacked.  Otherwise (windows too wide for the grouped kernel) k_fwd.
+template <typename T, int VB>
+int op_forward_chunk(admm_ctx* C, const T* img, T* sino, int nc, hipStream_t s) {
+  const int npix = C->npix, m = C->mrays;
+  int pl = 0, cus = 0;
+  RET((pick_fwd_plan<T, VB>(C, 1, &pl, &cus)));
+  if (C->op_nblk[pl] == 0) RET(build_fwd_order_into(C, pl, 1, cus, C->op_order[pl], &C->op_nblk[pl]));
+  T* xs = (T*)C->op_img.p;
+  T* xsT = (T*)C->op_imgT.p;
+  T* sI = (T*)C->op_sino.p;
+  hipLaunchKernelGGL((k_pack<T, VB>), dim3((npix + 255) / 256, 1), dim3(256), 0, s, img, xs, npix, nc);
+  CHECK_LAUNCH();
+  hipLaunchKernelGGL((k_transpose<T, VB>), tile_grid(C, 1, VB), dim3(kBlock), 0, s, (const T*)xs, xsT, C->g.N);
+  CHECK_LAUNCH();
+  RET((launch_fwdg_taps_with<T, VB>(C, xs, xsT, (T*)C->op_fpart.p, C->plan_groups[pl],
+                                    (const int4*)C->op_order[pl].p, C->op_nblk[pl], nc, s)));
+  hipLaunchKernelGGL((k_fwd_combine<T, VB, 0>), dim3((m + kBlock - 1) / kBlock, 1), dim3(kBlock), 0, s,
+                     (const T*)C->op_fpart.p, sI, (const T*)nullptr, (double*)nullptr, C->fang, C->g.n_det,
+                     C->g.n_angles, nc);
+  CHECK_LAUNCH();
+  hipLaunchKernelGGL((k_unpack<T, VB>), dim3((m + 255) / 256, 1), dim3(256), 0, s, (const T*)sI, sino, m, nc);
+  CHECK_LAUNCH();
+  return ADMM_OK;
+}
+
+template <typename T>
+int op_forward(admm_ctx* C, const T* img, T* sino, int nimg, hipStream_t s) {
+  const size_t npix = C->npix, m = C->mrays, ds = sizeof(T);
+  const int N = C->g.N;
+  if (C->plan_n[0] == 0) {  // no angle-group plan for this geometry: ray-per-thread kernel
+    RET(ensure(C->op_imgT, (size_t)nimg * npix * ds));
+    hipLaunchKernelGGL((k_transpose<T, 1>), tile_grid(C, nimg, 1), dim3(kBlock), 0, s, img, (T*)C->op_imgT.p, N);
+    CHECK_LAUNCH();
+    return launch_fwd<T, 1, 0>(C, img, (const T*)C->op_imgT.p, sino, nullptr, nullptr, nimg, s);
+  }
+  const int cmax = std::min(nimg, 8);
+  const int vbmax = vb_for(cmax);
+  RET(ensure(C->op_img, vbmax * npix * ds));
+  RET(ensure(C->op_imgT, vbmax * npix * ds));
+  RET(ensure(C->op_sino, vbmax * m * ds));
+  RET(ensure(C->op_fpart, (size_t)kFgSeg * vbmax * m * ds));
+  for (int v0 = 0; v0 < nimg; v0 += 8) {
+    const int nc = std::min(8, nimg - v0);
+    const T* in = img + (size_t)v0 * npix;
+    T* out = sino + (size_t)v0 * m;
+    RET(with_vb(vb_for(nc), [&](auto vbc) { return op_forward_chunk<T, decltype(vbc)::value>(C, in, out, nc, s); }));
+  }
+  return ADMM_OK;
+}
+
 }  // namespace
 
 // ============================================================================
@@ -619,7 +697,7 @@ int admm_ctx_destroy(admm_ctx* C) {
   (void)hipSetDevice(C->device);
   (void)hipDeviceSynchronize();
   free_graphs(C);
-  Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->bI, &C->fpart, &C->r, &C->c,
+  Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->op_sino, &C->op_fpart, &C->op_order[0], &C->op_order[1], &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->bI, &C->fpart, &C->r, &C->c,
                  &C->d2, &C->e2, &C->partH, &C->partS, &C->partD, &C->partE, &C->redH, &C->fg_order, &C->dsumS, &C->ats};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
@@ -637,22 +715,9 @@ int admm_project_fwd(admm_ctx* C, const void* img, void* sino, int nimg, void* s
   if (!C || !img || !sino) return fail(ADMM_E_INVALID, "null argument");
   if (nimg < 1 || nimg > C->max_images) return fail(ADMM_E_INVALID, "nimg out of range");
   hipStream_t s = (hipStream_t)stream;
-  const size_t ds = dsize(C->dtype);
-  RET(ensure(C->op_imgT, (size_t)nimg * C->npix * ds));
-  const dim3 tg = tile_grid(C, nimg, 1);
-  // operator API: node-major images = interleave width 1
-  if (C->dtype == ADMM_DTYPE_F32) {
-    hipLaunchKernelGGL((k_transpose<float, 1>), tg, dim3(kBlock), 0, s, (const float*)img, (float*)C->op_imgT.p,
-                       C->g.N);
-    CHECK_LAUNCH();
-    return launch_fwd<float, 1, 0>(C, (const float*)img, (const float*)C->op_imgT.p, (float*)sino, nullptr, nullptr,
-                                   nimg, s);
-  }
-  hipLaunchKernelGGL((k_transpose<double, 1>), tg, dim3(kBlock), 0, s, (const double*)img, (double*)C->op_imgT.p,
-                     C->g.N);
-  CHECK_LAUNCH();
-  return launch_fwd<double, 1, 0>(C, (const double*)img, (const double*)C->op_imgT.p, (double*)sino, nullptr,
-                                  nullptr, nimg, s);
+  HIPCHK(hipSetDevice(C->device));
+  return C->dtype == ADMM_DTYPE_F32 ? op_forward<float>(C, (const float*)img, (float*)sino, nimg, s)
+                                    : op_forward<double>(C, (const double*)img, (double*)sino, nimg, s);
 }
 
 int admm_project_adj(admm_ctx* C, const void* sino, void* img, int nimg, void* stream) {

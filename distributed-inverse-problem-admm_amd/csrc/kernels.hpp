@@ -1,7 +1,7 @@
 // kernels.hpp -- CDNA4 (gfx950) kernels of the decentralized-ADMM tomography hot path.
 //
 // Everything is batched over the graph nodes this GPU owns.  All nodes share one
-// parallel-beam geometry (block_2_load_odl_data.py:69: every node spans [0, pi)
+// parallel-beam geometry (block_2_load_odl_data.py:51: every node spans [0, pi)
 // with its own a angles), so one launch projects VB node images at once: the
 // per-step geometry (interpolation position, weights, clamped offsets) is computed
 // once and reused VB times.
@@ -216,7 +216,7 @@ __device__ __forceinline__ void block_reduce_rs(double (&v)[NV], double* lds /* 
 
 // ===========================================================================
 // Forward projector (Joseph, ray-driven):  sino[v][t][k] = sum_m L * interp(img_v, row m, l(m))
-// Replaces the ODL RayTransform `Ai @ x` (block_2_load_odl_data.py:72, dense form :86-114;
+// Replaces the ODL RayTransform `Ai @ x` (block_2_load_odl_data.py:54, dense form :68-96;
 // used at block_5_node_problem.py:21 and block_6_admm_loop_ver2.py:193).
 //
 // Block = 64 consecutive detector bins of one angle x 8 step segments (one wave each).
@@ -1557,6 +1557,19 @@ __global__ void k_pack(const T* __restrict__ in, T* __restrict__ out, int L, int
 #pragma unroll
   for (int u = 0; u < VB; ++u) s[u] = (v0 + u < V) ? in[(size_t)(v0 + u) * L + q] : T(0);
   gstore<T, VB>(out + ((size_t)chunk * L + q) * VB, s);
+}
+
+// interleaved [C][L][VB] samples -> node-major [V][L]  (grid.y = chunk)
+template <typename T, int VB>
+__global__ void k_unpack(const T* __restrict__ in, T* __restrict__ out, int L, int V) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  const int chunk = blockIdx.y, v0 = chunk * VB;
+  if (q >= L) return;
+  T s[VB];
+  gload<T, VB>(in + ((size_t)chunk * L + q) * VB, s);
+#pragma unroll
+  for (int u = 0; u < VB; ++u)
+    if (v0 + u < V) out[(size_t)(v0 + u) * L + q] = s[u];
 }
 
 // ===========================================================================

@@ -11,7 +11,7 @@
  *          (kwarg surface also of block_6_admm_loop.py:72-84)
  *
  * plus the operator they consume, the ODL ray transform materialised as a dense
- * matrix (block_2_load_odl_data.py:34-114), used only through `A @ x`,
+ * matrix (block_2_load_odl_data.py:16-96), used only through `A @ x`,
  * `A.T @ r` and column norms (block_6_admm_loop_ver2.py:145,193;
  * block_3_graph_and_precisions.py:20-23).  The Python drop-ins in
  * distributed-inverse-problem-admm_amd/ call the entry points below through
@@ -81,7 +81,7 @@ extern "C" {
 #define ADMM_EDGE_STATS 3
 
 /* Parallel-beam geometry of one graph node.  Replaces the ODL construction of
- * block_2_load_odl_data.py:34-83: space [-1,1]^2 (N x N), angles
+ * block_2_load_odl_data.py:16-65: space [-1,1]^2 (N x N), angles
  * uniform_partition(angle_min, angle_max, n_angles) midpoints, detector
  * uniform_partition(det_min, det_max, n_det) midpoints.  All nodes share it. */
 typedef struct admm_geom {

@@ -10,7 +10,7 @@ What it is: a NumPy/SciPy (float64 by default) restatement of the reference
 algorithm for the hot path named in BASELINE.json ``north_star``:
 
 * ``geometry``   -- ODL parallel-beam geometry of
-  ``/root/reference/block_2_load_odl_data.py:34-83`` (space [-1,1]^2, angles
+  ``/root/reference/block_2_load_odl_data.py:16-65`` (space [-1,1]^2, angles
   ``uniform_partition(0, pi, a)`` midpoints, detector
   ``uniform_partition(-1, 1, N)`` midpoints), discretised as a Joseph
   (ray-driven, linear interpolation) ray transform held as a sparse matrix.

@@ -2,12 +2,12 @@
 
 TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
 
-Geometry restated from /root/reference/block_2_load_odl_data.py:34-83:
-  * image space ``uniform_discr([-1,-1], [1,1], [N,N])`` (:41-46): pixel size
+Geometry restated from /root/reference/block_2_load_odl_data.py:16-65:
+  * image space ``uniform_discr([-1,-1], [1,1], [N,N])`` (:23-28): pixel size
     h = 2/N, pixel centres x_i = -1 + (i+1/2) h, axis 0 = x, axis 1 = y;
-  * angles ``uniform_partition(0, pi, a)`` (:69) -> midpoints (t+1/2) pi / a;
+  * angles ``uniform_partition(0, pi, a)`` (:51) -> midpoints (t+1/2) pi / a;
     every node spans the full half circle with its own ``a`` angles;
-  * detector ``uniform_partition(-w/2, w/2, N)`` (:60-70), w = 2*det_width_factor.
+  * detector ``uniform_partition(-w/2, w/2, N)`` (:42-44, :52), w = 2*det_width_factor.
 ODL Parallel2dGeometry defaults: detector axis at angle theta is
 (cos theta, sin theta) and rays run along (-sin theta, cos theta), so detector
 coordinate s sees the line  x cos(theta) + y sin(theta) = s.
@@ -31,15 +31,15 @@ import scipy.sparse as sp
 
 @dataclass(frozen=True)
 class Geometry:
-    """2-D parallel-beam geometry of one graph node (block_2_load_odl_data.py:34-83)."""
+    """2-D parallel-beam geometry of one graph node (block_2_load_odl_data.py:16-65)."""
 
     N: int
     n_angles: int
-    det_width_factor: float = 1.0  # block_2_load_odl_data.py:34,60
+    det_width_factor: float = 1.0  # block_2_load_odl_data.py:16,42
 
     @property
     def n_det(self) -> int:
-        return self.N  # det_pixels = N  (block_2_load_odl_data.py:62)
+        return self.N  # det_pixels = N  (block_2_load_odl_data.py:44)
 
     @property
     def h(self) -> float:
@@ -51,13 +51,13 @@ class Geometry:
 
     @property
     def angles(self) -> np.ndarray:
-        # uniform_partition(0, pi, a) midpoints (block_2_load_odl_data.py:69)
+        # uniform_partition(0, pi, a) midpoints (block_2_load_odl_data.py:51)
         t = np.arange(self.n_angles, dtype=np.float64)
         return (t + 0.5) * math.pi / self.n_angles
 
     @property
     def det_centers(self) -> np.ndarray:
-        # uniform_partition(-w/2, w/2, N) midpoints (block_2_load_odl_data.py:70)
+        # uniform_partition(-w/2, w/2, N) midpoints (block_2_load_odl_data.py:52)
         w = 2.0 * self.det_width_factor
         k = np.arange(self.n_det, dtype=np.float64)
         return -w / 2.0 + (k + 0.5) * self.h_det
@@ -68,7 +68,7 @@ class Geometry:
 
 
 def split_angles(angles_total: int, num_nodes: int) -> list[int]:
-    """Per-node angle counts, block_2_load_odl_data.py:49-56."""
+    """Per-node angle counts, block_2_load_odl_data.py:31-38."""
     per = [angles_total // num_nodes] * num_nodes
     for i in range(angles_total % num_nodes):
         per[i] += 1
@@ -76,15 +76,17 @@ def split_angles(angles_total: int, num_nodes: int) -> list[int]:
 
 
 def default_angles_total(N: int) -> int:
-    """block_2_load_odl_data.py:49-51: max(180, 3N)."""
+    """block_2_load_odl_data.py:31-33: max(180, 3N)."""
     return max(180, 3 * N)
 
 
-def joseph_matrix(geom: Geometry, dtype=np.float64) -> sp.csr_matrix:
+def joseph_matrix(geom: Geometry, dtype=np.float64, angles=None) -> sp.csr_matrix:
     """Joseph ray transform of ``geom`` as a CSR matrix (m x n).
 
     Row r = t*n_det + k (angle-major, C order, as the flattened sinogram of
     block_6_admm_loop_ver2.py:46); column = C-order pixel i*N + j.
+    ``angles`` (indices into the geometry's angle list) keeps only those angles'
+    rows, in the given order (len(angles)*n_det rows) -- large-N spot checks.
     """
     N = geom.N
     c0 = 0.5 * (N - 1)
@@ -92,15 +94,18 @@ def joseph_matrix(geom: Geometry, dtype=np.float64) -> sp.csr_matrix:
     cs, sn = np.cos(th), np.sin(th)
     s_idx = geom.det_centers / geom.h  # detector coordinate in pixel units
     rows_all, cols_all, vals_all = [], [], []
-    T, K = np.meshgrid(np.arange(geom.n_angles), np.arange(geom.n_det), indexing="ij")
+    tsel = np.arange(geom.n_angles) if angles is None else np.asarray(angles, dtype=np.int64)
+    T, K = np.meshgrid(tsel, np.arange(geom.n_det), indexing="ij")
+    R, _ = np.meshgrid(np.arange(len(tsel)), np.arange(geom.n_det), indexing="ij")
     T = T.ravel()
     K = K.ravel()
+    R = R.ravel()
     caseA = np.abs(cs[T]) >= np.abs(sn[T])
     alpha = np.where(caseA, cs[T], sn[T])
     beta = np.where(caseA, sn[T], cs[T])
     L = geom.h / np.abs(alpha)
     sk = s_idx[K]
-    row = T * geom.n_det + K
+    row = R * geom.n_det + K
     for m in range(N):
         l = c0 + (sk - (m - c0) * beta) / alpha
         i0 = np.floor(l)
@@ -119,7 +124,7 @@ def joseph_matrix(geom: Geometry, dtype=np.float64) -> sp.csr_matrix:
     rows = np.concatenate(rows_all)
     cols = np.concatenate(cols_all)
     vals = np.concatenate(vals_all).astype(dtype)
-    A = sp.coo_matrix((vals, (rows, cols)), shape=geom.shape).tocsr()
+    A = sp.coo_matrix((vals, (rows, cols)), shape=(len(tsel) * geom.n_det, N * N)).tocsr()
     A.sum_duplicates()
     return A
 

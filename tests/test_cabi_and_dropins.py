@@ -82,7 +82,7 @@ REF_SIGNATURES = {
         "eps_pri", "eps_dual", "verbose", "scs_total_iters", "scs_chunk_iters", "scs_snapshot_dir",
         "scs_use_indirect", "scs_eps", "scs_alpha", "scs_acceleration", "scs_lookback", "scs_scale",
         "scs_save_every_chunks"],
-    # /root/reference/block_2_load_odl_data.py:117-127
+    # /root/reference/block_2_load_odl_data.py:99-109
     ("block_2_load_odl_data", "load_odl_data"): [
         "N", "num_nodes", "noise_level", "output_dir", "make_plots", "show_plots", "phantom_array",
         "save_operators_dir", "build_dense"],

@@ -75,7 +75,7 @@ def test_numpy_roundtrip_and_batch_of_one(cuda):
 
 
 def test_detector_wider_than_image(cuda):
-    """det_width_factor > 1 (block_2_load_odl_data.py:34,60): rays outside the image are 0."""
+    """det_width_factor > 1 (block_2_load_odl_data.py:16,42): rays outside the image are 0."""
     g = Geometry(40, 30, det_width_factor=1.5)
     A = joseph_matrix(g)
     op = RayTransform(ParallelBeamGeometry(40, 30, det_width_factor=1.5), "float64")

@@ -20,7 +20,7 @@ def rel(a, b):
     return float(np.linalg.norm(np.asarray(a) - np.asarray(b)) / np.linalg.norm(np.asarray(b)))
 
 
-# ---------------- geometry (block_2_load_odl_data.py:34-83) ----------------
+# ---------------- geometry (block_2_load_odl_data.py:16-65) ----------------
 def test_angle_split_and_defaults():
     assert default_angles_total(64) == 192 and default_angles_total(32) == 180
     assert split_angles(192, 5) == [39, 39, 38, 38, 38]
