@@ -20,14 +20,14 @@ ADMM_TV_ANISO = 1
 ADMM_FUSE_MIDPOINT = 0
 ADMM_FUSE_WEIGHTED = 1
 ADMM_BATCH_KEEP_X = 1  # admm_batch.flags: x_ext local rows written only by admm_node_update
-ABI_VERSION = 2
+ABI_VERSION = 3
 ADMM_MASK_KNN = 0
 ADMM_MASK_MST = 1
 ADMM_MASK_CHAIN = 2
 ADMM_Q_ARITHMETIC = 0
 ADMM_Q_HARMONIC = 1
 MASK_MAX_NODES = 64
-NODE_STATS = 5  # mse_sino, |g|^2, TV, quad, img
+NODE_STATS = 6  # mse_sino, |g|^2, TV, quad, img, split-Bregman stationarity residual^2
 EDGE_STATS = 3  # |x_a-z|^2, |x_b-z|^2, |dz|^2
 
 
@@ -102,6 +102,7 @@ SYMBOLS = {
     "admm_batch_bind": [C.c_void_p, C.POINTER(Batch)],
     "admm_batch_atb": [C.c_void_p, C.c_void_p, C.c_void_p],
     "admm_node_update": [C.c_void_p, C.c_void_p],
+    "admm_node_update_rounds": [C.c_void_p, C.c_int, C.c_void_p],
     "admm_consensus": [C.c_void_p, C.c_void_p],
     "admm_time_forward": [C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_double)],
     "admm_pixel_masks": [C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_void_p,

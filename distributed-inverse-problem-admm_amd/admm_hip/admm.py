@@ -9,7 +9,19 @@ the node solves and edge updates on the GPU:
       z/y update + residual partials -> NodeBatch.consensus     (:210-253)
       statistics -> history, stop test                          (:189-206,255-289)
 
-Histories carry the reference's keys (:310-326).  One process per GPU: when
+Histories carry the reference's keys (:310-326), plus ``sb_res_history`` (the
+split-Bregman stationarity residual ||A^T(Ax-b) + rho(Dx-c) + mu K^T e|| of each
+accepted x) and ``inner_updates_history`` (x-updates spent per node).
+
+Inner-solve control (row a5).  Default (``inner_tol=None``): one fixed-count x-update
+(tv_iters x cg_iters) per node per iteration, deterministic; ``eps_used_history`` is NaN
+because no tolerance is applied.  ``inner_tol="reference"``: the accept / tighten loop of
+:100-176 -- the node is solved to eps_try = min(1e-2, eps_target(k)) (repeated warm
+x-updates until its split-Bregman residual <= eps_try, at most ``max_inner_updates`` per
+solve, standing in for SCS's tolerance), accepted if the reference's ||g|| <= eps_target,
+else eps_try /= 5 and re-solved, at most twice, then force-accepted; eps_used is the
+eps_try of the accepted iterate.  Other nodes' state is untouched while one node
+re-solves (masked batch updates).  One process per GPU: when
 ``torch.distributed`` is initialised with world size > 1 the graph nodes are
 sharded (plan.py) and every rank returns the same ``(x_list, history)``.
 """
@@ -34,7 +46,10 @@ HISTORY_KEYS = (
     "g_norm_history", "eps_used_history", "eps_target_history",
 )
 
+EXTRA_KEYS = ("sb_res_history", "inner_updates_history")
+
 DEFAULT_MU_FACTOR = 10.0  # split-Bregman penalty mu = 10 * lam_tv
+EPS_CAP, CALIB_ALPHA, MAX_TIGHTEN = 1e-2, 1.0, 2  # block_6_admm_loop_ver2.py:106-113
 
 
 def eps_target(k: int) -> float:
@@ -71,7 +86,20 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
              max_iters=10, eps_pri=1e-1, eps_dual=1e-1, verbose=True, snapshot_dir=None,
              snapshot_every=None, snapshot_div=10, phantom_true=None, mu=None, tv_iters=10,
              cg_iters=5, tv_kind="iso", group=None, return_tensors=False, timing=None,
-             write_params=True, fusion="midpoint"):
+             write_params=True, fusion="midpoint", inner_tol=None, max_inner_updates=10,
+             inner_chunks=None, chunk_snapshot_dir=None, chunk_save_every=1):
+    """``inner_chunks``: split each x-update into warm-started solves of these round counts
+    (block_6_admm_loop.py:14-69 chunked SCS); ``chunk_snapshot_dir`` then receives that
+    file's per-chunk snapshots (``_chunk_snapshot``) every ``chunk_save_every`` chunks."""
+    if inner_tol not in (None, "reference"):
+        raise ValueError("inner_tol must be None (fixed counts) or 'reference'")
+    if inner_chunks is not None:
+        inner_chunks = [int(r) for r in inner_chunks]
+        if not inner_chunks or min(inner_chunks) < 1:
+            raise ValueError("inner_chunks must be a non-empty list of positive round counts")
+        if inner_tol is not None:
+            raise ValueError("inner_chunks and inner_tol are exclusive")
+        tv_iters = inner_chunks[0]
     V_total = len(A_dense_list)
     geom, dtype, device = _common_geometry(A_dense_list)
     if geom.N != N:
@@ -90,11 +118,12 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
         snapshot_every = max(1, max_iters // snapshot_div)  # _ver2:31-32
     nb = NodeBatch(geom, dtype, plan, sinograms, Qij_diag_fn, rho, lam_tv, mu, tv_iters, cg_iters,
                    tv_kind, phantom_true, device, fusion=fusion, Wi_list=Wi_list,
-                   keep_x=True)  # this loop never writes x itself
+                   keep_x=inner_tol is None)  # this loop never writes x itself (masked
+    # re-solves of the tolerance mode restore x rows, so that mode re-projects x)
     halo = HaloExchange(plan, nb.x_ext, group)
     if world > 1:
         dist.barrier(group=group)
-    hist = {k: [] for k in HISTORY_KEYS}
+    hist = {k: [] for k in HISTORY_KEYS + EXTRA_KEYS}
     edges = plan.edges
     have_ph = phantom_true is not None
     if verbose and rank == 0:
@@ -106,21 +135,36 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
         t_loop = time.perf_counter()
     iters_done = 0
     for k in range(max_iters):
-        nb.node_update()
+        et = eps_target(k)
+        if inner_chunks is None:
+            nb.node_update()
+        else:
+            for cid, rounds in enumerate(inner_chunks):
+                nb.node_update(rounds=rounds)
+                if chunk_snapshot_dir is not None and cid % int(chunk_save_every) == 0:
+                    _chunk_snapshot(chunk_snapshot_dir, k, cid, plan, nb.x_local, N)
+        eps_used = np.full(plan.V, np.nan)
+        n_upd = np.ones(plan.V)
+        if inner_tol == "reference":
+            eps_used, n_upd = _solve_to_reference_tolerance(nb, et, max_inner_updates)
         halo.run()
         nb.consensus()
-        ns, es = assemble_stats(plan, nb.node_stats, nb.edge_stats[: len(plan.stored_edges)], group)
+        extra = torch.as_tensor(np.stack([eps_used, n_upd], axis=1), dtype=torch.float64,
+                                device=nb.node_stats.device)
+        ns, es = assemble_stats(plan, torch.cat([nb.node_stats, extra], dim=1),
+                                nb.edge_stats[: len(plan.stored_edges)], group)
         ns = ns.numpy()
         es = es.numpy()
         iters_done = k + 1
         # --- node diagnostics (_ver2:145-206) ---
-        et = eps_target(k)
         mse = ns[:, 0].copy()
         g_norm = np.sqrt(ns[:, 1])
         obj = 0.5 * ns[:, 0] + lam_tv * ns[:, 2] + ns[:, 3]
         hist["g_norm_history"].append(g_norm)
-        hist["eps_used_history"].append(np.full(V_total, min(1e-2, et)))
+        hist["eps_used_history"].append(ns[:, 6].copy())
         hist["eps_target_history"].append(np.full(V_total, et))
+        hist["sb_res_history"].append(np.sqrt(ns[:, 5]))
+        hist["inner_updates_history"].append(ns[:, 7].astype(np.int64))
         hist["mse_sino_per_node"].append(mse)
         hist["mse_sino_total"].append(float(np.sum(mse)))
         img = ns[:, 4].copy() if have_ph else np.full(V_total, np.nan)
@@ -169,16 +213,67 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
     return [Xh[i].copy() for i in range(V_total)], hist
 
 
-def _snapshot(snapshot_dir, k, plan, x_local, N):
-    """_ver2:269-281: iter_XXXX_node_i.npy (C-order reshape) + .png."""
-    it_tag = f"iter_{k + 1:04d}"
+def _solve_to_reference_tolerance(nb, et, max_inner_updates):
+    """block_6_admm_loop_ver2.py:105-176 for every local node (after its first x-update):
+    solve to eps_try, accept if ||g|| <= eps_target, else tighten eps_try /= 5 (<= 2 times)."""
+    V = nb.V
+    eps_try = np.full(V, min(EPS_CAP, CALIB_ALPHA * et))
+    tries = np.zeros(V, dtype=np.int64)
+    n_upd = np.ones(V)
+    active = np.ones(V, dtype=bool)
+    st = nb.node_stats.to("cpu").numpy()
+    while True:
+        g, sb = np.sqrt(st[:, 1]), np.sqrt(st[:, 5])
+        need = active & (sb > eps_try) & (n_upd < (tries + 1) * max_inner_updates)
+        if need.any():  # keep solving the nodes not yet at their eps_try
+            nb.node_update_masked(need)
+            n_upd += need
+            st = nb.node_stats.to("cpu").numpy()
+            continue
+        done = active & ((g <= et) | (tries >= MAX_TIGHTEN))  # accepted or forced (:155-172)
+        active &= ~done
+        if not active.any():
+            return eps_try, n_upd
+        tries[active] += 1
+        eps_try[active] /= 5.0  # :174-176
+
+
+def _chunk_snapshot(out_dir, k, cid, plan, x_local, N):
+    """block_6_admm_loop.py:55-66: {out_dir}/node_{i}/node_{i}_outer_{k}_chunk_{c}.npy holding
+    x.reshape(N, N, order="F") (the skeleton's Fortran-order image), + .png."""
     xs = x_local.to("cpu").numpy()
+    plt = _pyplot()
+    for r, g in enumerate(plan.local_nodes):
+        d = os.path.join(out_dir, f"node_{g}")
+        os.makedirs(d, exist_ok=True)
+        tag = f"node_{g}_outer_{k}"
+        img = xs[r].reshape(N, N, order="F")
+        np.save(os.path.join(d, f"{tag}_chunk_{cid}.npy"), img)
+        if plt is not None:
+            plt.figure(figsize=(5, 5))
+            plt.imshow(img, cmap="gray")
+            plt.title(f"{tag} after chunk {cid}")
+            plt.axis("off")
+            plt.tight_layout()
+            plt.savefig(os.path.join(d, f"{tag}_chunk_{cid}.png"), dpi=220)
+            plt.close()
+
+
+def _pyplot():
     try:
         import matplotlib
         matplotlib.use("Agg")
         import matplotlib.pyplot as plt
+        return plt
     except Exception:  # pragma: no cover
-        plt = None
+        return None
+
+
+def _snapshot(snapshot_dir, k, plan, x_local, N):
+    """_ver2:269-281: iter_XXXX_node_i.npy (C-order reshape) + .png."""
+    it_tag = f"iter_{k + 1:04d}"
+    xs = x_local.to("cpu").numpy()
+    plt = _pyplot()
     for r, g in enumerate(plan.local_nodes):
         img = xs[r].reshape(N, N)
         np.save(os.path.join(snapshot_dir, f"{it_tag}_node_{g}.npy"), img)

@@ -67,6 +67,14 @@ def _torch():
     return torch
 
 
+def default_device() -> int:
+    """The calling process's current HIP device (torch.cuda.current_device()): with one
+    process per GPU and ``torch.cuda.set_device(local_rank)`` first, every operator a rank
+    builds lands on its own GPU.  0 when no GPU is visible (host-only logic, tests)."""
+    torch = _torch()
+    return int(torch.cuda.current_device()) if torch.cuda.is_available() else 0
+
+
 def current_stream_handle(device=None) -> int:
     torch = _torch()
     return int(torch.cuda.current_stream(device).cuda_stream)
@@ -122,12 +130,12 @@ class RayTransform:
     (k images) and returns the same kind; ``A.T @ y`` is the exact adjoint.
     """
 
-    def __init__(self, geom: ParallelBeamGeometry, dtype: str = "float32", device: int = 0):
+    def __init__(self, geom: ParallelBeamGeometry, dtype: str = "float32", device: int | None = None):
         if dtype not in ("float32", "float64"):
             raise ValueError("dtype must be float32 or float64")
         self.geom = geom
         self.dtype = dtype
-        self.device = device
+        self.device = default_device() if device is None else int(device)
         self.shape = (geom.m, geom.n)
         self._adjoint = False
 

@@ -24,6 +24,9 @@ Q_MODES = {"arithmetic": _lib.ADMM_Q_ARITHMETIC, "harmonic": _lib.ADMM_Q_HARMONI
 
 
 def _stack_w(Wi_list, device) -> torch.Tensor:
+    if device is None:
+        from .geometry import default_device
+        device = default_device()
     dev = torch.device("cuda", device)
     rows = [(w if isinstance(w, torch.Tensor) else torch.as_tensor(np.asarray(w))).reshape(-1)
             for w in Wi_list]
@@ -46,7 +49,7 @@ def chain_orders(V: int, n: int, seed: int = 0) -> np.ndarray:
 
 
 def pixel_masks(Wi_list, strategy: str = "knn", k: int = 2, seed: int = 0,
-                q_mode: str = "arithmetic", device: int = 0) -> torch.Tensor:
+                q_mode: str = "arithmetic", device: int | None = None) -> torch.Tensor:
     """keep[i, j, p] (uint8, device) of _build_all_pixel_masks (block_3:154-187)."""
     if strategy not in STRATEGIES:
         raise ValueError("strategy must be one of 'knn', 'mst', or 'chain'")

@@ -156,8 +156,33 @@ class NodeBatch:
     def x_local(self) -> torch.Tensor:
         return self.x_ext[: self.plan.V]
 
-    def node_update(self) -> None:
-        _lib.check(self.lib.admm_node_update(self.ctx.h, C.c_void_p(self._s())), "admm_node_update")
+    def node_update(self, rounds: int | None = None) -> None:
+        """One x-update of every local node; ``rounds`` overrides the bound split-Bregman
+        round count (chunked solves, admm_node_update_rounds)."""
+        if rounds is None:
+            _lib.check(self.lib.admm_node_update(self.ctx.h, C.c_void_p(self._s())), "admm_node_update")
+        else:
+            _lib.check(self.lib.admm_node_update_rounds(self.ctx.h, int(rounds), C.c_void_p(self._s())),
+                       "admm_node_update_rounds")
+
+    def node_update_masked(self, active) -> None:
+        """x-update of the nodes where ``active`` (bool, length V) is set; the others keep
+        their x, d, e and statistics bitwise (saved before, restored after the batched
+        update).  Needs keep_x=False: a restored node's x no longer matches the kept
+        A^T(Ax - b) of the reuse start."""
+        act = torch.as_tensor(np.asarray(active, dtype=bool))
+        if bool(act.all()):
+            self.node_update()
+            return
+        if not bool(act.any()):
+            return
+        if self.cb.flags & _lib.ADMM_BATCH_KEEP_X:
+            raise RuntimeError("node_update_masked needs a batch bound with keep_x=False")
+        idx = torch.nonzero(~act).reshape(-1).to(self.dev)
+        saved = [(t, t.index_select(0, idx)) for t in (self.x_local, self.d, self.e, self.node_stats)]
+        self.node_update()
+        for t, s in saved:
+            t.index_copy_(0, idx, s)
 
     def consensus(self) -> None:
         if self.plan.stored_edges:
@@ -181,9 +206,12 @@ class NodeBatch:
 
 
 def make_operators(N: int, num_nodes: int, angles_total: int | None = None, dtype: str = "float32",
-                   device: int = 0, det_width_factor: float = 1.0) -> list[RayTransform]:
-    """Per-node ray transforms of block_2_load_odl_data.py:16-65 (all nodes span [0, pi))."""
-    from .geometry import split_angles
+                   device: int | None = None, det_width_factor: float = 1.0) -> list[RayTransform]:
+    """Per-node ray transforms of block_2_load_odl_data.py:16-65 (all nodes span [0, pi)),
+    on ``device`` (default: the current device, see geometry.default_device)."""
+    from .geometry import default_device, split_angles
+    if device is None:
+        device = default_device()
     if angles_total is None:
         angles_total = max(180, 3 * N)
     per = split_angles(angles_total, num_nodes)

@@ -35,7 +35,8 @@ def build_pixel_connected_Q_provider(base_dir="saved_operators_Incmp_Span",
                 "(pickled dense matrices); pass ops=<RayTransform list> or Wi_list= instead")
         Wi_list, _ = make_precisions(ops, q_mode=q_mode)
     if device is None:
-        device = ops[0].device if ops is not None else 0
+        from admm_hip.geometry import default_device
+        device = ops[0].device if ops is not None else default_device()
     keep = pixel_masks(Wi_list, strategy=strategy, k=k, seed=seed, q_mode=q_mode, device=device)
     G_union = None
     if plot_union:

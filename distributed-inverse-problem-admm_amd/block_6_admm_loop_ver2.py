@@ -12,6 +12,12 @@ updates run on MI355X (admm_hip.admm.run_admm).  Extra keyword arguments:
                 or "weighted" (z = (W_i a_i + W_j a_j)/(W_i + W_j) with W = Wi_list, the
                 form commented out at :221-222 and ADMM_Algo.pdf eq.(2))
 
+* ``inner_tol``  None (default: fixed tv_iters x cg_iters per x-update, deterministic) or
+                "reference" (the accept / tighten loop of :100-176: solve to
+                eps_try = min(1e-2, eps_target), accept if ||g|| <= eps_target, else
+                eps_try /= 5, at most twice; see admm_hip/admm.py)
+* ``max_inner_updates``  x-updates per tolerance solve in "reference" mode (default 10)
+
 ``max_inner_iters`` is accepted and, as in the reference, unused.
 """
 from __future__ import annotations
@@ -26,7 +32,8 @@ def decentralized_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn,
                        verbose=True, snapshot_dir=None,
                        snapshot_every=None, snapshot_div=10, phantom_true=None,
                        mu=None, tv_iters=10, cg_iters=5, tv_kind="iso", group=None,
-                       write_params=True, fusion="midpoint"):
+                       write_params=True, fusion="midpoint", inner_tol=None,
+                       max_inner_updates=10):
     """Returns (x_list, history) like block_6_admm_loop_ver2.py:310-326."""
     del max_inner_iters  # accepted but unused, as in the reference (_ver2:17)
     return run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=lam_tv, rho=rho,
@@ -34,4 +41,5 @@ def decentralized_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn,
                     snapshot_dir=snapshot_dir, snapshot_every=snapshot_every,
                     snapshot_div=snapshot_div, phantom_true=phantom_true, mu=mu,
                     tv_iters=tv_iters, cg_iters=cg_iters, tv_kind=tv_kind, group=group,
-                    write_params=write_params, fusion=fusion)
+                    write_params=write_params, fusion=fusion, inner_tol=inner_tol,
+                    max_inner_updates=max_inner_updates)

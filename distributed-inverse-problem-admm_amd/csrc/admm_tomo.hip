@@ -283,7 +283,7 @@ int launch_reduce(const double* part, int rows, int P, double* out, int G, int o
 // the x-update sequence for the bound batch (replaces block_6_admm_loop_ver2.py:81-197)
 // --------------------------------------------------------------------------
 template <typename T, int VB>
-int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false) {
+int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 0) {
   const admm_batch& B = C->b;
   const int V = B.V, N = C->g.N;
   const size_t npix = (size_t)N * N;
@@ -346,7 +346,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false) {
   double* ecur = B.e;
   double* dnxt = (double*)C->d2.p;
   double* enxt = (double*)C->e2.p;
-  const int K = B.cg_iters, Tt = B.tv_iters;
+  const int K = B.cg_iters, Tt = rounds > 0 ? rounds : B.tv_iters;
   for (int t = 0; t < Tt; ++t) {
     for (int kk = 0; kk < K; ++kk) {
       RET((launch_fwd_batch<T, VB, 0>(C, p, pT, sino, nullptr, nullptr, V, s)));
@@ -408,17 +408,18 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false) {
     a.lam = B.lam;
     a.mu = B.mu;
     a.tv_kind = B.tv_kind;
+    a.evar = B.e;  // the final Bregman variable (copied back from scratch above for odd rounds)
     a.out_t = (B.flags & ADMM_BATCH_KEEP_X) ? (T*)C->ats.p : nullptr;
     RET((launch_back<T, VB, BACK_DIAG>(C, a, V, s)));
   }
   RET(launch_reduce((double*)C->partS.p, V, C->P_fwd, B.node_stats, 1, ADMM_NODE_STATS, ADMM_NODE_STAT_MSE_SINO, s));
-  RET(launch_reduce((double*)C->partD.p, 4 * V, Pb, B.node_stats, 4, ADMM_NODE_STATS, ADMM_NODE_STAT_G2, s));
+  RET(launch_reduce((double*)C->partD.p, 5 * V, Pb, B.node_stats, 5, ADMM_NODE_STATS, ADMM_NODE_STAT_G2, s));
   return ADMM_OK;
 }
 
 template <typename T>
-int enqueue_update_any(admm_ctx* C, hipStream_t s, bool reuse = false) {
-  return with_vb(C->vb, [&](auto vbc) { return enqueue_update<T, decltype(vbc)::value>(C, s, reuse); });
+int enqueue_update_any(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 0) {
+  return with_vb(C->vb, [&](auto vbc) { return enqueue_update<T, decltype(vbc)::value>(C, s, reuse, rounds); });
 }
 
 int enqueue_consensus(admm_ctx* C, hipStream_t s) {
@@ -825,7 +826,7 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   C->P_edge = (int)((npix + kBlock * 4 - 1) / (kBlock * 4));
   RET(ensure(C->partH, (size_t)5 * V * C->P_back * 8));
   RET(ensure(C->partS, (size_t)V * C->P_fwd * 8));
-  RET(ensure(C->partD, (size_t)4 * V * C->P_back * 8));
+  RET(ensure(C->partD, (size_t)5 * V * C->P_back * 8));
   RET(ensure(C->partE, (size_t)3 * std::max(1, B.n_edges) * C->P_edge * 8));
   RET(ensure(C->redH, (size_t)5 * V * 8));
   C->bound = true;
@@ -888,6 +889,20 @@ int admm_node_update(admm_ctx* C, void* stream) {
                                     : enqueue_update_any<double>(C, s, reuse);
   }
   if (rc == ADMM_OK && keep) C->ats_valid = true;  // this update's DIAG left A^T s of its x
+  return rc;
+}
+
+int admm_node_update_rounds(admm_ctx* C, int tv_iters, void* stream) {
+  if (!C || !C->bound) return fail(ADMM_E_STATE, "no batch bound");
+  if (tv_iters < 1) return fail(ADMM_E_INVALID, "tv_iters must be >= 1");
+  if (tv_iters == C->b.tv_iters) return admm_node_update(C, stream);
+  hipStream_t s = (hipStream_t)stream;
+  const bool keep = (C->b.flags & ADMM_BATCH_KEEP_X) != 0;
+  const bool reuse = keep && C->ats_valid;
+  // a round count other than the bound one: enqueued directly (no recorded graph)
+  const int rc = C->dtype == ADMM_DTYPE_F32 ? enqueue_update_any<float>(C, s, reuse, tv_iters)
+                                            : enqueue_update_any<double>(C, s, reuse, tv_iters);
+  if (rc == ADMM_OK && keep) C->ats_valid = true;
   return rc;
 }
 

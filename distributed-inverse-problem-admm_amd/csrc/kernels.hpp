@@ -656,7 +656,8 @@ __global__ __launch_bounds__(kBlock) void k_fwd_combine(const T* __restrict__ pa
 //   BACK_H     : Hp = A^T A p + rho D p + mu K^T K p; partials p.Hp, r.Hp, Hp.Hp, r.r, r.p (CG)
 //   BACK_INIT  : r = A^T b + rho c + mu K^T(d-e) - H xs;  p = r                      (CG start)
 //   BACK_DIAG  : g = A^T s + rho (D x - c) + lam K^T sub(Kx); partials |g|^2, TV(x),
-//                sum_j rho/2 q_ij (x - v_ij)^2, |x - phantom|^2   (block_6_ver2.py:135-149)
+//                sum_j rho/2 q_ij (x - v_ij)^2, |x - phantom|^2   (block_6_ver2.py:135-149),
+//                |A^T s + rho (D x - c) + mu K^T e|^2 (split-Bregman stationarity residual)
 // ===========================================================================
 enum BackMode { BACK_PLAIN = 0, BACK_ATB = 1, BACK_WSQ = 2, BACK_H = 3, BACK_INIT = 4, BACK_DIAG = 5 };
 
@@ -679,7 +680,7 @@ struct BackArgs {
   const double* atb;        // INIT
   const double* cvec;       // INIT, DIAG: c = sum_j q v
   const double* dvar;       // INIT: d [V][2][n]
-  const double* evar;       // INIT: e [V][2][n]
+  const double* evar;       // INIT, DIAG: e [V][2][n]
   const double* x;          // DIAG: x rows of x_ext
   const double* phantom;    // DIAG (may be null)
   const double* yv;         // DIAG: edge y [E][n]
@@ -871,7 +872,7 @@ constexpr int kBAngC = ADMM_BK_ANGC;  // angles per staged sinogram-window chunk
 template <typename T, int VB>
 __device__ __forceinline__ void diag_epilogue_tile(const BackArgs<T>& A, double* scratch, int ib, int jb, int i,
                                                    int j, bool inb, int chunk, int v0, int nv, const T (&acc)[VB],
-                                                   double (&pq)[VB][4]) {
+                                                   double (&pq)[VB][5]) {
   constexpr int XC = kBTJ + 2, XR = kBTI + 2, SC = kBTJ + 1, SR = kBTI + 1;
   double* xt = scratch;            // [XR][XC]: rows ib-1 .. ib+kBTI, cols jb-1 .. jb+kBTJ
   double* sx = xt + XR * XC;       // [SR][SC]: subgradient at rows ib-1 .. ib+kBTI-1, cols jb-1 ..
@@ -920,7 +921,16 @@ __device__ __forceinline__ void diag_epilogue_tile(const BackArgs<T>& A, double*
     if (i >= 1) kts += sx[(ti - 1) * SC + tj];
     if (j >= 1) kts += sy[ti * SC + tj - 1];
     const double cc = A.cvec[vo + pix];
-    const double g = (double)acc[u] + A.rho * (A.dsum[vo + pix] * xc - cc) + A.lam * kts;
+    const double sm = (double)acc[u] + A.rho * (A.dsum[vo + pix] * xc - cc);  // gradient of the quadratic
+    const double g = sm + A.lam * kts;
+    // K^T e at (i, j) (e = final Bregman variable [2][n] of node v)
+    const double* ev = A.evar + 2 * vo;
+    double kte = 0.0;
+    if (i >= 1) kte += ev[pix - N];
+    if (i <= N - 2) kte -= ev[pix];
+    if (j >= 1) kte += ev[npix + pix - 1];
+    if (j <= N - 2) kte -= ev[npix + pix];
+    const double rsb = sm + A.mu * kte;
     double quad = 0.0;
     for (int q = A.inc_off[v]; q < A.inc_off[v + 1]; ++q) {
       const size_t eo = (size_t)A.inc_edge[q] * npix + pix;
@@ -935,12 +945,13 @@ __device__ __forceinline__ void diag_epilogue_tile(const BackArgs<T>& A, double*
       const double dp = xc - A.phantom[pix];
       pq[u][3] += dp * dp;
     }
+    pq[u][4] += rsb * rsb;
   }
 }
 
 template <typename T, int VB, int MODE>
 __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
-  constexpr int NQ = (MODE == BACK_H) ? 5 : (MODE == BACK_DIAG) ? 4 : 1;
+  constexpr int NQ = (MODE == BACK_H) ? 5 : (MODE == BACK_DIAG) ? 5 : 1;
   constexpr int NPL = Planes<T, VB>::NPL, PV = Planes<T, VB>::PV;
   const int N = A.N, n_det = A.n_det, n_ang = A.n_ang;
   const int m_rays = n_ang * n_det;

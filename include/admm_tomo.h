@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ADMM_ABI_VERSION 2
+#define ADMM_ABI_VERSION 3
 
 #define ADMM_OK 0
 #define ADMM_E_INVALID (-1)
@@ -72,7 +72,9 @@ extern "C" {
 #define ADMM_NODE_STAT_TV 2       /* TV(x)                   (block_4_tv_helpers.py:5-14) */
 #define ADMM_NODE_STAT_QUAD 3     /* sum_j rho/2 ||x-v_ij||^2_Q (block_5_node_problem.py:26-29) */
 #define ADMM_NODE_STAT_IMG 4      /* ||x - phantom||^2       (block_6_admm_loop_ver2.py:199-204) */
-#define ADMM_NODE_STATS 5
+#define ADMM_NODE_STAT_SBRES2 5   /* ||A^T(Ax-b) + rho(D x - c) + mu K^T e||^2: stationarity of eq.(1)
+                                     with the split-Bregman dual p = mu e / lam (ABI 3) */
+#define ADMM_NODE_STATS 6
 
 /* per-edge statistics written by admm_consensus (float64) */
 #define ADMM_EDGE_STAT_RA2 0 /* ||x_a - z||^2 */
@@ -171,6 +173,11 @@ int admm_batch_atb(admm_ctx* ctx, double* atb_out, void* stream);
  * fixed-count split-Bregman/CG solve of eq.(1), diagnostics into node_stats.
  * Replaces block_6_admm_loop_ver2.py:81-197 (build_node_problem + SCS + g check). */
 int admm_node_update(admm_ctx* ctx, void* stream);
+/* admm_node_update with `tv_iters` split-Bregman rounds instead of the bound count
+ * (warm-started from the current x, d, e: k calls of r rounds continue one solve of
+ * k*r rounds up to rounding).  The chunked solves of block_6_admm_loop.py:14-69
+ * (_scs_solve_in_chunks) use it between snapshots.  ABI 3. */
+int admm_node_update_rounds(admm_ctx* ctx, int tv_iters, void* stream);
 /* Edge updates z = (a_i + a_j)/2 (or the W-weighted mean, ADMM_FUSE_WEIGHTED),
  * y += x - z at both ends, and the residual partial sums
  * into edge_stats.  Replaces block_6_admm_loop_ver2.py:210-253.  Every edge

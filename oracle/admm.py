@@ -6,6 +6,10 @@ of ``node_solver`` (fixed-count split-Bregman + CG instead of CVXPY+SCS):
   * state init x=0, z=0, y=0 (:35-43); b_i = sinograms[i].reshape(-1) (:46)
   * neighbour gather v_ij = z_ij - y_ij,i, q_ij = Qij_diag_fn(i,j) (:85-95)
   * eps_target = 2/(k+1)^1.005, first SCS eps = min(1e-2, eps_target) (:101-108)
+  * inner_tol="reference": the accept / tighten loop of :110-176 -- an inner solve to
+    eps_try (x-updates until the split-Bregman stationarity residual <= eps_try, at most
+    max_inner_updates), accept if ||g|| <= eps_target, else eps_try /= 5, at most two
+    tightenings, then force-accept; eps_used = the eps_try of the accepted iterate
   * z_ij = (a_i + a_j)/2 with a = x + y (:210-223); y += x - z (:225-230)
   * fusion="weighted": z_ij = (W_i a_i + W_j a_j)/(W_i + W_j), the form the
     code comments at :216-222 and ADMM_Algo.pdf eq.(2) give
@@ -35,6 +39,8 @@ HISTORY_KEYS = (
     "mse_sino_per_node", "mse_sino_total", "img_mse_per_node", "img_mse_total",
     "g_norm_history", "eps_used_history", "eps_target_history",
 )
+EXTRA_KEYS = ("sb_res_history", "inner_updates_history")
+EPS_CAP, CALIB_ALPHA, MAX_TIGHTEN = 1e-2, 1.0, 2  # block_6_admm_loop_ver2.py:106-113
 
 
 def canonical_edges(G) -> list[tuple[int, int]]:
@@ -73,13 +79,20 @@ def edge_update_literal(G, x, y, z, Wi_list=None):
 def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
                        max_iters=10, eps_pri=1e-1, eps_dual=1e-1, phantom_true=None,
                        mu=None, tv_iters=10, cg_iters=5, tv_kind="iso",
-                       dtype=np.float64, node_subset=None, fusion="midpoint", Wi_list=None):
+                       dtype=np.float64, node_subset=None, fusion="midpoint", Wi_list=None,
+                       inner_tol=None, max_inner_updates=10, node_map=None):
     """Oracle ADMM.  ``ops`` = list of scipy sparse matrices (one per node).
 
     Returns (x_list, history) with the reference's history keys.  With
     ``node_subset`` only those nodes' x-updates run (the others keep x=0); used
     only to time a bounded CPU sample.  ``fusion="weighted"`` needs ``Wi_list``.
+    ``node_map(tasks)`` (fixed-count mode only) runs the iteration's independent node
+    updates -- a list of (i, b_i, D, c, qv, state, N, params, dtype) -- and returns
+    [(state, diag)] in order (oracle/parallel.py: one process per node, Jacobi order,
+    so results equal the sequential loop).
     """
+    if node_map is not None and inner_tol is not None:
+        raise ValueError("node_map runs fixed-count updates only")
     if fusion not in ("midpoint", "weighted"):
         raise ValueError("fusion must be 'midpoint' or 'weighted'")
     weighted = fusion == "weighted"
@@ -94,14 +107,19 @@ def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
                         tv_kind=tv_kind)
     edges = canonical_edges(G)
     b = [np.asarray(s, dtype=np.float64).reshape(-1) for s in sinograms]
-    ATs = [A.T.tocsr() for A in ops]
+    # scipy matrices; any object with @ and .T (e.g. the GPU RayTransform, used by the
+    # full-size tests as an operator-level oracle: this loop's float64 vector algebra
+    # around a projector that is itself checked against joseph_matrix)
+    ATs = [A.T.tocsr() if hasattr(A.T, "tocsr") else A.T for A in ops]
     Atb = [ATs[i] @ b[i] for i in range(V)]
     states = [ns.NodeState.zeros(n, dtype) for _ in range(V)]
     y = {e: np.zeros(n) for e in edges}
     z = {e: np.zeros(n) for e in edges}
     y2 = {e: np.zeros(n) for e in edges} if weighted else None
     nbrs = {i: list(G.neighbors(i)) for i in range(V)}
-    hist = {k: [] for k in HISTORY_KEYS}
+    if inner_tol not in (None, "reference"):
+        raise ValueError("inner_tol must be None or 'reference'")
+    hist = {k: [] for k in HISTORY_KEYS + EXTRA_KEYS}
     ph = None
     if phantom_true is not None:
         ph = np.asarray(phantom_true, dtype=np.float64).reshape(-1)
@@ -110,8 +128,13 @@ def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
         obj_i = np.zeros(V)
         g_i = np.zeros(V)
         mse_i = np.zeros(V)
+        sb_i = np.zeros(V)
+        # eps_used: the tolerance the accepted iterate was solved to (NaN for fixed counts)
+        eu_i = np.full(V, min(EPS_CAP, CALIB_ALPHA * eps_target(k)) if inner_tol else np.nan)
+        nu_i = np.zeros(V, dtype=np.int64)
         et = eps_target(k)
         todo = range(V) if node_subset is None else node_subset
+        tasks = []
         for i in todo:
             qv = []
             D = np.zeros(n)
@@ -124,14 +147,38 @@ def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
                 D += q
                 c += q * v
                 qv.append((q, v))
+            if node_map is not None:
+                tasks.append((i, b[i], D, c, qv, states[i], N, prm, dtype))
+                continue
             d = ns.node_update(ops[i], Atb[i], b[i], D, c, qv, states[i], N, prm, dtype=dtype,
                                AT=ATs[i])
+            nu_i[i] = 1
+            if inner_tol == "reference":
+                eps_try, tries = eu_i[i], 0
+                while True:
+                    while d.sb_res > eps_try and nu_i[i] < (tries + 1) * max_inner_updates:
+                        d = ns.node_update(ops[i], Atb[i], b[i], D, c, qv, states[i], N, prm,
+                                           dtype=dtype, AT=ATs[i])
+                        nu_i[i] += 1
+                    if d.g_norm <= et or tries >= MAX_TIGHTEN:
+                        break
+                    tries += 1
+                    eps_try /= 5.0
+                eu_i[i] = eps_try
             obj_i[i] = d.obj
+            sb_i[i] = d.sb_res
             g_i[i] = d.g_norm
             mse_i[i] = d.mse_sino
+        if node_map is not None:
+            for (i, *_), (st, d) in zip(tasks, node_map(tasks)):
+                states[i] = st
+                nu_i[i] = 1
+                obj_i[i], sb_i[i], g_i[i], mse_i[i] = d.obj, d.sb_res, d.g_norm, d.mse_sino
         x = [st.x.astype(np.float64) for st in states]
         hist["g_norm_history"].append(g_i)
-        hist["eps_used_history"].append(np.full(V, min(1e-2, et)))
+        hist["eps_used_history"].append(eu_i)
+        hist["sb_res_history"].append(sb_i)
+        hist["inner_updates_history"].append(nu_i)
         hist["eps_target_history"].append(np.full(V, et))
         hist["mse_sino_per_node"].append(mse_i)
         hist["mse_sino_total"].append(float(np.sum(mse_i)))

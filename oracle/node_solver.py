@@ -61,6 +61,7 @@ class NodeDiag:
     obj: float = 0.0
     mse_sino: float = 0.0
     g_norm: float = 0.0
+    sb_res: float = 0.0  # ||A^T s + rho (D x - c) + mu K^T e||: stationarity with p = mu e / lam
     tv: float = 0.0
     quad: float = 0.0
     cg_rr: list = field(default_factory=list)
@@ -129,6 +130,8 @@ def node_update(A, Atb, b, D, c, qv_terms, st: NodeState, N: int, p: NodeParams,
     diag.mse_sino = _dot(s, s)
     g = cast(AT @ s) + cast(rho * (D * x - c)) + cast(lam * tvmod.subgrad(x, N, p.tv_kind))
     diag.g_norm = float(np.sqrt(_dot(g, g)))
+    rsb = cast(AT @ s) + cast(rho * (D * x - c)) + cast(mu * tvmod.div_t(st.ex, st.ey, N))
+    diag.sb_res = float(np.sqrt(_dot(rsb, rsb)))
     diag.tv = tvmod.tv_value(x.astype(np.float64), N, p.tv_kind)
     quad = 0.0
     for q, v in qv_terms:

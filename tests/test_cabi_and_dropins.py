@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
         assert name in _lib.SYMBOLS, f"{name} not bound in _lib.SYMBOLS"
     assert set(_lib.SYMBOLS) == set(names)
-    assert lib.admm_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.admm_abi_version() == _lib.ABI_VERSION == 3
 
 
 def test_error_path_without_gpu_work():
@@ -99,6 +99,9 @@ REF_DEFAULTS = {
                                                            eps_dual=1e-1, verbose=True, snapshot_div=10),
     ("block_6_admm_loop", "decentralized_admm"): dict(lam_tv=0.01, rho=1.0, max_iters=200, eps_pri=1e-3,
                                                       eps_dual=1e-3, scs_total_iters=100),
+    # /root/reference/block_2_load_odl_data.py:99-109
+    ("block_2_load_odl_data", "load_odl_data"): dict(N=128, num_nodes=5, noise_level=0.005,
+                                                     build_dense=True),
 }
 
 

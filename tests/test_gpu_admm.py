@@ -76,8 +76,8 @@ def compare(G, N, V, iters, angles_total, dtype="float32", tol=1e-5, tv_kind="is
     for k in ("obj_total", "mse_sino_total", "img_mse_total"):
         assert errs[k] < max(10 * tol, 1e-4), (k, errs)
     # |g| contains the TV subgradient K^T(Kx/|Kx|), discontinuous where |Kx| ~ 0 (flat
-    # phantom regions): image differences of 1e-7 move it by ~1e-4.  Diagnostic only.
-    assert errs["g"] < max(100 * tol, 2e-3), errs
+    # phantom regions): image differences of 1e-7 move it by ~1e-5.  Diagnostic only.
+    assert errs["g"] < max(20 * tol, 2e-4), errs  # measured <= 2.4e-5 (C1, 20 iterations)
     return x, h, xo, ho
 
 

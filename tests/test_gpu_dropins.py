@@ -1,0 +1,164 @@
+"""GPU: the setup and output drop-ins and the tolerance-driven
+inner solve (row a5).
+
+* f1 ``load_odl_data`` (block_2_load_odl_data.py:99-253): keys, operators on the current
+  device, A_i x vs the oracle Joseph matrix, noise level, column norms, aggregate
+  sinogram (A_agg phantom_0 + noise with build_dense, :160-177; stacked otherwise, :159).
+* f4 writers: ``_ver2`` snapshots iter_XXXX_node_i.npy (C-order reshape, :269-281) and
+  admm_internal_params.txt (:291-306); the skeleton's chunked-solve snapshots
+  {dir}/node_i/node_i_outer_k_chunk_c.npy (Fortran-order reshape, block_6_admm_loop.py:55-66).
+* a5 ``inner_tol="reference"``: GPU histories equal the oracle's and obey the
+  reference's accept / tighten rule (block_6_admm_loop_ver2.py:100-176).
+"""
+import os
+
+import networkx as nx
+import numpy as np
+import pytest
+import torch
+
+from admm_hip.data import make_precisions, make_sinograms, shepp_logan
+from admm_hip.solver import make_operators
+from block_2_load_odl_data import load_odl_data
+import block_6_admm_loop
+from block_6_admm_loop_ver2 import decentralized_admm
+from oracle import admm as oadmm
+from oracle.geometry import Geometry, joseph_matrix
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+@pytest.mark.parametrize("build_dense", [True, False])
+def test_load_odl_data_matches_reference_contract(cuda, tmp_path, build_dense):
+    N, V = 128, 4
+    d = load_odl_data(N=N, num_nodes=V, noise_level=0.005, output_dir=str(tmp_path / "out"),
+                      build_dense=build_dense)
+    assert set(d) == {"A_dense_list", "sinograms", "column_norms_all", "N", "num_nodes",
+                      "agg_ray_trafo", "A_agg", "agg_sinogram", "output_dir", "phantom", "phantoms"}
+    assert os.path.isdir(d["output_dir"])
+    a_tot = max(180, 3 * N)  # :31-33
+    a = a_tot // V
+    ops = d["A_dense_list"]
+    assert len(ops) == V and all(A.device == torch.cuda.current_device() for A in ops)
+    assert all(A.shape == (a * N, N * N) for A in ops)
+    ph = d["phantom"]
+    assert ph.dtype == np.float32 and ph.shape == (N, N) and len(d["phantoms"]) == V
+    Ao = joseph_matrix(Geometry(N, a))
+    clean = Ao @ ph.astype(np.float64).ravel()
+    for i, s in enumerate(d["sinograms"]):
+        assert s.shape == (a, N) and s.dtype == np.float32
+        r = s.astype(np.float64).ravel() - clean
+        assert abs(r.std() - 0.005) < 0.0005 and abs(r.mean()) < 0.0005, (i, r.std(), r.mean())
+    W = np.maximum(np.asarray(Ao.multiply(Ao).sum(axis=0)).ravel(), 1e-12)
+    for cn in d["column_norms_all"]:
+        assert rel(cn ** 2, W) < 2e-6
+    agg = d["agg_sinogram"]
+    if build_dense:
+        assert d["A_agg"] is d["agg_ray_trafo"]
+        assert agg.shape == (a_tot, N)
+        Aagg = joseph_matrix(Geometry(N, a_tot))
+        r = agg.astype(np.float64).ravel() - Aagg @ ph.astype(np.float64).ravel()
+        assert abs(r.std() - 0.005) < 0.0005
+        assert rel(d["agg_ray_trafo"] @ ph.ravel(), Aagg @ ph.astype(np.float64).ravel()) < 2e-6
+    else:
+        assert d["A_agg"] is None
+        assert np.array_equal(agg, np.vstack(d["sinograms"]))
+
+
+def _small(N=32, V=4):
+    ops = make_operators(N, V, 180, device=0)
+    ph = shepp_logan(N)
+    sinos = make_sinograms(ops, ph, 0.005, seed=1000)
+    Wi, Q = make_precisions(ops)
+    return ops, ph.numpy(), sinos, Wi, Q
+
+
+def test_ver2_snapshots_and_params_file(cuda, tmp_path):
+    N, V = 32, 4
+    ops, ph, sinos, Wi, Q = _small(N, V)
+    out = tmp_path / "snaps"
+    x, h = decentralized_admm(ops, sinos, nx.cycle_graph(V), Wi, Q, N, lam_tv=0.02, rho=2.0,
+                              max_iters=6, eps_pri=0.0, eps_dual=0.0, verbose=False,
+                              snapshot_dir=str(out), snapshot_every=3)
+    for it in (3, 6):
+        for i in range(V):
+            f = out / f"iter_{it:04d}_node_{i}.npy"
+            assert f.exists() and (out / f"iter_{it:04d}_node_{i}.png").exists()
+    assert not (out / "iter_0001_node_0.npy").exists()
+    for i in range(V):  # last snapshot == returned image, C-order reshape (_ver2:273)
+        img = np.load(out / f"iter_0006_node_{i}.npy", allow_pickle=False)
+        assert img.shape == (N, N) and np.array_equal(img, x[i].reshape(N, N))
+    txt = (out / "admm_internal_params.txt").read_text().splitlines()
+    assert txt[0] == "===== ADMM Internal Parameters ====="
+    assert txt[1] == "rho = 2.0" and txt[2] == "lambda_tv = 0.02" and txt[3] == f"Number of nodes = {V}"
+    # snapshot_every default: max(1, max_iters // snapshot_div) (_ver2:31-32)
+    out2 = tmp_path / "snaps2"
+    decentralized_admm(ops, sinos, nx.cycle_graph(V), Wi, Q, N, lam_tv=0.02, rho=2.0, max_iters=4,
+                       eps_pri=0.0, eps_dual=0.0, verbose=False, snapshot_dir=str(out2),
+                       snapshot_div=2, write_params=False)
+    assert sorted(p.name for p in out2.glob("*.npy")) == sorted(
+        f"iter_{it:04d}_node_{i}.npy" for it in (2, 4) for i in range(V))
+
+
+def test_skeleton_chunked_snapshots_fortran_order(cuda, tmp_path):
+    """block_6_admm_loop.py: scs_total_iters=50 -> 10 rounds of 5 CG steps, chunks of
+    scs_chunk_iters=20 -> 4 rounds (4, 4, 2); snapshots every 2nd chunk, F-order."""
+    N, V = 32, 3
+    ops, ph, sinos, Wi, Q = _small(N, V)
+    out = tmp_path / "chunks"
+    x, h = block_6_admm_loop.decentralized_admm(ops, sinos, nx.cycle_graph(V), Wi, Q, N, lam_tv=0.02,
+                                                rho=2.0, max_iters=2, eps_pri=0.0, eps_dual=0.0,
+                                                verbose=False, scs_total_iters=50, scs_chunk_iters=20,
+                                                scs_snapshot_dir=str(out), scs_save_every_chunks=2,
+                                                write_params=False)
+    for i in range(V):
+        names = sorted(p.name for p in (out / f"node_{i}").glob("*.npy"))
+        assert names == sorted(f"node_{i}_outer_{k}_chunk_{c}.npy" for k in (0, 1) for c in (0, 2))
+        last = np.load(out / f"node_{i}" / f"node_{i}_outer_1_chunk_2.npy", allow_pickle=False)
+        assert np.array_equal(last, x[i].reshape(N, N, order="F"))
+    # the chunked solve continues one 10-round solve (restarts only recompute r exactly)
+    x1, h1 = decentralized_admm(ops, sinos, nx.cycle_graph(V), Wi, Q, N, lam_tv=0.02, rho=2.0,
+                                max_iters=2, eps_pri=0.0, eps_dual=0.0, verbose=False,
+                                tv_iters=10, write_params=False)
+    assert rel(np.stack(x), np.stack(x1)) < 1e-6
+    # unchunked: no snapshot files, as in the reference (:127-134)
+    out2 = tmp_path / "nochunk"
+    block_6_admm_loop.decentralized_admm(ops, sinos, nx.cycle_graph(V), Wi, Q, N, max_iters=1,
+                                         verbose=False, scs_snapshot_dir=str(out2), write_params=False)
+    assert not out2.exists() or not list(out2.rglob("*.npy"))
+
+
+def test_reference_tolerance_mode_matches_oracle_and_rule(cuda):
+    N, V, iters = 32, 4, 6
+    ops, ph, sinos, Wi, Q = _small(N, V)
+    G = nx.cycle_graph(V)
+    x, h = decentralized_admm(ops, sinos, G, Wi, Q, N, lam_tv=0.02, rho=2.0, max_iters=iters,
+                              eps_pri=0.0, eps_dual=0.0, verbose=False, phantom_true=ph,
+                              write_params=False, inner_tol="reference")
+    A = joseph_matrix(Geometry(N, 45))
+    xo, ho = oadmm.decentralized_admm([A] * V, [s.double().cpu().numpy() for s in sinos], G, Q, N,
+                                      lam_tv=0.02, rho=2.0, max_iters=iters, eps_pri=0.0,
+                                      eps_dual=0.0, phantom_true=ph, inner_tol="reference")
+    assert rel(np.stack(x), np.stack(xo)) < 1e-5
+    assert rel(h["primal"], ho["primal"]) < 1e-5
+    eu, eo = np.stack(h["eps_used_history"]), np.stack(ho["eps_used_history"])
+    assert np.array_equal(eu, eo), (eu, eo)
+    assert np.array_equal(np.stack(h["inner_updates_history"]), np.stack(ho["inner_updates_history"]))
+    et = np.stack(h["eps_target_history"])
+    g = np.stack(h["g_norm_history"])
+    first = np.minimum(1e-2, et)
+    # accepted (||g|| <= eps_target) or force-accepted after exactly two tightenings (:155-176)
+    ok = (g <= et) | np.isclose(eu, first / 25.0, rtol=1e-12)
+    assert ok.all(), (g, et, eu)
+    assert (np.isclose(eu, first / 25.0)).any() and (g <= et).any()  # both branches exercised
+    assert (np.stack(h["inner_updates_history"]) > 1).any()  # the inner solve to eps_try ran
+    # default mode: one fixed-count update per node, no tolerance -> eps_used NaN
+    _, hd = decentralized_admm(ops, sinos, G, Wi, Q, N, lam_tv=0.02, rho=2.0, max_iters=2,
+                               eps_pri=0.0, eps_dual=0.0, verbose=False, write_params=False)
+    assert np.isnan(np.stack(hd["eps_used_history"])).all()
+    assert (np.stack(hd["inner_updates_history"]) == 1).all()

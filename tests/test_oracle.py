@@ -191,7 +191,7 @@ def test_admm_golden_trajectory():
     assert rel(np.stack(x), GOLD["admm_x"]) < 1e-12
     for k in ("primal", "dual", "obj_total", "mse_sino_total", "img_mse_total"):
         assert rel(h[k], GOLD[f"admm_{k}"]) < 1e-10, k
-    assert set(h) == set(oadmm.HISTORY_KEYS)
+    assert set(h) == set(oadmm.HISTORY_KEYS) | set(oadmm.EXTRA_KEYS)
 
 
 def test_single_y_form_equals_reference_two_dual_form():

@@ -133,7 +133,7 @@ def run_sharded(rank, world, gname, HaloExchange, assemble_stats, gather_images,
     halo = HaloExchange(plan, x_ext)
     hist = {"primal": [], "dual": [], "obj": []}
     for k in range(3):
-        node_stats = torch.zeros((plan.V, 5), dtype=torch.float64)
+        node_stats = torch.zeros((plan.V, 6), dtype=torch.float64)
         for r, g in enumerate(plan.local_nodes):
             D = np.zeros(n)
             c = np.zeros(n)
@@ -146,7 +146,7 @@ def run_sharded(rank, world, gname, HaloExchange, assemble_stats, gather_images,
                 qv.append((W, v))
             d = ons.node_update(A, A.T @ sinos[g], sinos[g], D, c, qv, states[g], N, prm)
             x_ext[r] = torch.from_numpy(states[g].x)
-            node_stats[r] = torch.tensor([d.mse_sino, d.g_norm ** 2, d.tv, d.quad, 0.0])
+            node_stats[r] = torch.tensor([d.mse_sino, d.g_norm ** 2, d.tv, d.quad, 0.0, d.sb_res ** 2])
         halo.run()
         xs = x_ext.numpy()
         edge_stats = torch.zeros((max(E, 1), 3), dtype=torch.float64)
@@ -200,3 +200,45 @@ def test_gloo_sharded_matches_single_process_bitwise(gname, world):
     assert np.abs(np.stack(xo) - X1).max() <= 1e-10 * np.abs(X1).max()
     assert np.allclose(ho["primal"], h1["primal"], rtol=1e-7, atol=0)
     assert np.allclose(ho["dual"], h1["dual"], rtol=1e-7, atol=0)
+
+
+def _placement_rank(rank, world, port, q):
+    """INTEGRATION.md's recipe on a rank: torch.cuda.set_device(local_rank) before building
+    anything.  No GPU here, so the current-device query stands in for it (monkeypatched
+    per rank); only host-side construction runs (operators are lazy, nothing launches)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.is_available = lambda: True
+        torch.cuda.current_device = lambda: rank  # what set_device(local_rank) leaves behind
+        from admm_hip.geometry import ParallelBeamGeometry, RayTransform
+        from admm_hip.solver import make_operators
+        ops = make_operators(64, 4)
+        one = RayTransform(ParallelBeamGeometry(64, 45))
+        q.put((rank, [A.device for A in ops] + [one.device, one.T.device]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_operators_follow_each_ranks_current_device():
+    """Operators default to the caller's current device, so N ranks after
+    torch.cuda.set_device(local_rank) build on N different GPUs (not all on GPU 0)."""
+    import inspect
+    import block_2_load_odl_data
+    from admm_hip.geometry import RayTransform
+    from admm_hip.solver import make_operators
+    assert inspect.signature(make_operators).parameters["device"].default is None
+    assert inspect.signature(RayTransform).parameters["device"].default is None
+    assert inspect.signature(block_2_load_odl_data.load_odl_data).parameters["device"].default is None
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_placement_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == {0: [0] * 6, 1: [1] * 6}
