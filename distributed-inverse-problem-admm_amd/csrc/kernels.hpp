@@ -393,6 +393,9 @@ constexpr int kFgSeg = ADMM_FG_SEG;    // row segments (partial sums) per ray
 #ifndef ADMM_FG_W4
 #define ADMM_FG_W4 1  // chunk window origins as one int4 LDS read into scalars (0: one read per row)
 #endif
+#ifndef ADMM_FG_IDLE_SKIP
+#define ADMM_FG_IDLE_SKIP 1  // waves beyond the group's angle count skip the tap loop (0: tuning A/B)
+#endif
 #ifndef ADMM_FG_EO
 #define ADMM_FG_EO 1  // even/odd half-window LDS layout (0: plain pixel order, tuning only)
 #endif
@@ -524,7 +527,9 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
 #endif
   if (ADMM_FG_EXPT != 2) fetch(m_lo);
   for (int m0 = m_lo; m0 < m_hi; m0 += kFgRows) {
-    const int rows = (ADMM_FG_EXPT == 1) ? 0 : min(kFgRows, m_hi - m0);
+    // waves g >= G (groups smaller than kFgG) only stage and meet the barriers: their taps
+    // would repeat angle G-1's and burn the LDS bandwidth the real taps are bound by
+    const int rows = (ADMM_FG_EXPT == 1 || (ADMM_FG_IDLE_SKIP && g >= G)) ? 0 : min(kFgRows, m_hi - m0);
     // the chunk's window origins, read once into scalar registers (a per-row LDS read
     // would put a dependent LDS round trip in front of every row's tap reads)
     int wl[kFgRows];
