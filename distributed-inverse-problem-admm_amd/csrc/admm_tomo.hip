@@ -117,6 +117,8 @@ namespace {
     if (_rc != ADMM_OK) return _rc; \
   } while (0)
 
+constexpr int kXcds = 8;  // MI355X: 8 XCDs, workgroups dealt round-robin (id % 8)
+
 int vb_for(int V) { return V >= 5 ? 8 : (V >= 3 ? 4 : (V == 2 ? 2 : 1)); }
 
 void select_fwd_plan(admm_ctx* C, int pl) {
@@ -142,9 +144,35 @@ int build_fwd_order_into(admm_ctx* C, int pl, int nch, int cus, Buf& buf, int* n
       for (int s = 0; s < kFgSeg; ++s)
         for (int kc = 0; kc < gv[gi].nkc[s]; ++kc) v.push_back({make_int4(kc, gi, s + kFgSeg * c, 0), gv[gi].G});
   const int n = (int)v.size();
-  if (cus > 0) {  // cus <= 0: launch order = table order (tuning comparison)
-    std::stable_sort(v.begin(), v.end(), [](const Blk& a, const Blk& b) { return a.w > b.w; });
-    if (n <= 2 * cus && n > cus) std::reverse(v.begin() + cus, v.end());
+  const char* xe = getenv("ADMM_FWD_XCD");
+  const bool xcd = !(xe && xe[0] == '0');
+  auto by_weight = [](std::vector<Blk>& l, int slots) {
+    std::stable_sort(l.begin(), l.end(), [](const Blk& a, const Blk& b) { return a.w > b.w; });
+    const int m = (int)l.size();
+    if (m <= 2 * slots && m > slots) std::reverse(l.begin() + slots, l.end());
+  };
+  if (cus > 0 && xcd && cus % kXcds == 0) {
+    // XCD-aware: workgroups are dealt round-robin over the 8 XCDs (id % 8), so launch
+    // position p runs on XCD p % 8.  Row segment s goes to XCD s % 8: each XCD's L2 then
+    // holds one band of image rows (and of the transposed copy) instead of re-fetching the
+    // whole image from the Infinity Cache (LDS-DMA staging reads ~10x the image per launch).
+    // Per XCD: heaviest first, the second round reversed (heavy + light per CU pair).
+    std::vector<std::vector<Blk>> L(kXcds);
+    for (const Blk& b : v) L[(b.b.z % kFgSeg) % kXcds].push_back(b);
+    for (auto& l : L) by_weight(l, cus / kXcds);
+    std::vector<size_t> pos(kXcds, 0);
+    v.clear();
+    for (int p = 0; p < n; ++p) {
+      int x = p % kXcds;
+      if (pos[x] >= L[x].size()) {  // this XCD's segment is used up: the fullest list lends
+        size_t best = 0;
+        for (int y = 0; y < kXcds; ++y)
+          if (L[y].size() - pos[y] > best) best = L[y].size() - pos[y], x = y;
+      }
+      v.push_back(L[x][pos[x]++]);
+    }
+  } else if (cus > 0) {  // cus <= 0: launch order = table order (tuning comparison)
+    by_weight(v, cus);
   }
   std::vector<int4> t(n);
   for (int i = 0; i < n; ++i) t[i] = v[i].b;

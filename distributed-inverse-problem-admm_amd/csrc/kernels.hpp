@@ -393,6 +393,12 @@ constexpr int kFgSeg = ADMM_FG_SEG;    // row segments (partial sums) per ray
 #ifndef ADMM_FG_W4
 #define ADMM_FG_W4 1  // chunk window origins as one int4 LDS read into scalars (0: one read per row)
 #endif
+#ifndef ADMM_FG_DMA
+#define ADMM_FG_DMA 1  // LDS-DMA staging of 16-byte sample planes (0: register staging)
+#endif
+#ifndef ADMM_FG_PIPE
+#define ADMM_FG_PIPE 1  // software-pipelined taps of full chunks in the LDS-DMA kernel (0: row by row)
+#endif
 #ifndef ADMM_FG_IDLE_SKIP
 #define ADMM_FG_IDLE_SKIP 1  // waves beyond the group's angle count skip the tap loop (0: tuning A/B)
 #endif
@@ -454,7 +460,13 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   const int m_lo = seg * N / kFgSeg, m_hi = (seg + 1) * N / kFgSeg;
   const int nrows = m_hi - m_lo;
 
-  __shared__ Pack<T, PV> win[NPL][kFgRows][kFgRow];
+  // LDS-DMA staging (ADMM_FG_DMA): 16-byte sample planes land straight in LDS from a buffer
+  // resource per staged row (out-of-image columns are out-of-range offsets: zero-filled by the
+  // hardware, scripts/probes/dma_oob.hip), two chunk buffers, one barrier per chunk, and no
+  // VGPRs or ds_write instructions spent on staging.  float64 x 8 nodes (4 planes) keeps the
+  // register-staged single buffer (two would not fit two blocks per CU).
+  constexpr bool kDma = ADMM_FG_DMA && sizeof(Pack<T, PV>) == 16 && NPL <= 2;
+  __shared__ Pack<T, PV> win[kDma ? 2 : 1][NPL][kFgRows][kFgRow];
   // every row window of the segment (N <= 4096): origin and the width actually touched
   __shared__ __align__(16) int wlo_s[(4096 + kFgSeg - 1) / kFgSeg + 4];  // +4: int4 reads of the last chunk
   __shared__ int wnum_s[(4096 + kFgSeg - 1) / kFgSeg + 4];
@@ -481,40 +493,6 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   }
   __syncthreads();
 
-  // staging in two halves: issue global loads for chunk c+1 into registers
-  // (prefetch), compute chunk c from LDS, then write the registers into LDS.
-  Pack<T, PV> stage[PER];
-  auto fetch = [&](int m0) {
-    const int rows = min(kFgRows, m_hi - m0);
-#pragma unroll
-    for (int e = 0; e < PER; ++e) {
-      const int q = threadIdx.x + e * kFgThreads;
-      const int pl = q % NPL, rw = q / NPL;
-      const int r = rw / kFgWin, w = rw - r * kFgWin;
-      // only the row's touched width is fetched (the rest of the window is never read)
-      // both reads unconditional (in bounds: +4 padding), so they issue together
-      const int wn = wnum_s[m0 - m_lo + r], wo = wlo_s[m0 - m_lo + r];
-      const int col = (r < rows && w < wn) ? wo + w : -1;
-      if (q < kFgRows * kFgWin * NPL && col >= 0 && col < N) {
-        stage[e] = *reinterpret_cast<const Pack<T, PV>*>(src + ((size_t)(m0 + r) * N + col) * VB + pl * PV);
-      } else {
-#pragma unroll
-        for (int z = 0; z < PV; ++z) stage[e].v[z] = T(0);
-      }
-    }
-  };
-  auto commit = [&]() {
-#pragma unroll
-    for (int e = 0; e < PER; ++e) {
-      const int q = threadIdx.x + e * kFgThreads;
-      if (q < kFgRows * kFgWin * NPL) {
-        const int pl = q % NPL, rw = q / NPL;
-        const int r = rw / kFgWin, w = rw - r * kFgWin;
-        win[pl][r][ADMM_FG_EO ? ((w & 1) ? kFgOdd + (w >> 1) : (w >> 1)) : w] = stage[e];
-      }
-    }
-  };
-
   // float samples: ray position l = l0 + m dl advanced per row in 32.32 fixed point
   // (|error| <= rows * 2^-33 pixel, below the float32 weights' own rounding)
   long long lfix = llrint(fma((double)m_lo, a.dl, l0) * 4294967296.0);
@@ -525,14 +503,10 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
 #ifndef ADMM_FG_EXPT
 #define ADMM_FG_EXPT 0  // timing diagnostics only: 1 = no tap loop, 2 = no staging
 #endif
-  if (ADMM_FG_EXPT != 2) fetch(m_lo);
-  for (int m0 = m_lo; m0 < m_hi; m0 += kFgRows) {
-    // waves g >= G (groups smaller than kFgG) only stage and meet the barriers: their taps
-    // would repeat angle G-1's and burn the LDS bandwidth the real taps are bound by
-    const int rows = (ADMM_FG_EXPT == 1 || (ADMM_FG_IDLE_SKIP && g >= G)) ? 0 : min(kFgRows, m_hi - m0);
-    // the chunk's window origins, read once into scalar registers (a per-row LDS read
-    // would put a dependent LDS round trip in front of every row's tap reads)
-    int wl[kFgRows];
+  int wl_cur[kFgRows];  // the current chunk's window origins (scalars)
+  // the chunk's window origins, read once into scalar registers (a per-row LDS read
+  // would put a dependent LDS round trip in front of every row's tap reads)
+  auto origins = [&](int m0, int (&wl)[kFgRows]) {
     if constexpr (ADMM_FG_W4 && kFgRows == 4) {
       const int4 w4 = *reinterpret_cast<const int4*>(&wlo_s[m0 - m_lo]);
       wl[0] = __builtin_amdgcn_readfirstlane(w4.x);
@@ -543,13 +517,9 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
 #pragma unroll
       for (int r = 0; r < kFgRows; ++r) wl[r] = wlo_s[m0 - m_lo + r];
     }
-    __syncthreads();  // previous chunk's readers are done
-    if (ADMM_FG_EXPT != 2) commit();
-    __syncthreads();
-    if (ADMM_FG_PRIO == 1) __builtin_amdgcn_s_setprio(1);
-    if (ADMM_FG_EXPT != 2 && m0 + kFgRows < m_hi) fetch(m0 + kFgRows);
-    if (ADMM_FG_PRIO == 1) __builtin_amdgcn_s_setprio(0);
-    if (ADMM_FG_PRIO == 2) __builtin_amdgcn_s_setprio(1);
+  };
+  // the taps of one staged chunk: every row's two taps per ray from LDS
+  auto taps = [&](const Pack<T, PV> (&wb)[NPL][kFgRows][kFgRow], int m0, int rows, const int (&wl)[kFgRows]) {
 #pragma unroll
     for (int r = 0; r < kFgRows; ++r) {  // unrolled: the chunk's LDS reads can all be in flight
       if (r >= rows) break;
@@ -583,8 +553,8 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       }
 #pragma unroll
       for (int q = 0; q < NPL; ++q) {
-        const Pack<T, PV> s0 = win[q][r][se];
-        const Pack<T, PV> s1 = win[q][r][so];
+        const Pack<T, PV> s0 = wb[q][r][se];
+        const Pack<T, PV> s1 = wb[q][r][so];
 #pragma unroll
         for (int e = 0; e < PV; ++e) {
           acc[q * PV + e] = fma(we, s0.v[e], acc[q * PV + e]);
@@ -592,7 +562,156 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         }
       }
     }
-    if (ADMM_FG_PRIO == 2) __builtin_amdgcn_s_setprio(0);
+  };
+  // Software-pipelined full chunk (ADMM_FG_PIPE): every row's tap slots and weights first,
+  // then row r+1's LDS reads issued before row r's FMAs, so one row's reads are always in
+  // flight behind the other's arithmetic (the LDS-DMA staging freed the registers: the
+  // register-staged kernel had no room for the second row's 16).  Same FMAs, same order.
+  auto taps4 = [&](const Pack<T, PV> (&wb)[NPL][kFgRows][kFgRow], int m0) {
+    int se[kFgRows], so[kFgRows];
+    T we[kFgRows], wo[kFgRows];
+#pragma unroll
+    for (int r = 0; r < kFgRows; ++r) {
+      int idx;
+      T w1;
+      if constexpr (std::is_same<T, float>::value) {
+        idx = (int)(lfix >> 32) - wl_cur[r];
+        w1 = (float)(unsigned)lfix * 2.3283064365386963e-10f;
+        lfix += dlfix;
+      } else {
+        const double l = fma((double)(m0 + r), a.dl, l0);
+        const double fl = floor(l);
+        idx = (int)fl - wl_cur[r];
+        w1 = (T)(l - fl);
+      }
+      const T w0 = T(1) - w1;
+      const bool odd = idx & 1;
+      se[r] = (idx + 1) >> 1;
+      so[r] = kFgOdd + (idx >> 1);
+      we[r] = odd ? w1 : w0;
+      wo[r] = odd ? w0 : w1;
+    }
+    Pack<T, PV> cur[2 * NPL], nxt[2 * NPL];
+#pragma unroll
+    for (int q = 0; q < NPL; ++q) {
+      cur[2 * q] = wb[q][0][se[0]];
+      cur[2 * q + 1] = wb[q][0][so[0]];
+    }
+#pragma unroll
+    for (int r = 0; r < kFgRows; ++r) {
+      if (r + 1 < kFgRows) {
+#pragma unroll
+        for (int q = 0; q < NPL; ++q) {
+          nxt[2 * q] = wb[q][r + 1][se[r + 1]];
+          nxt[2 * q + 1] = wb[q][r + 1][so[r + 1]];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < NPL; ++q)
+#pragma unroll
+        for (int e = 0; e < PV; ++e) {
+          acc[q * PV + e] = fma(we[r], cur[2 * q].v[e], acc[q * PV + e]);
+          acc[q * PV + e] = fma(wo[r], cur[2 * q + 1].v[e], acc[q * PV + e]);
+        }
+#pragma unroll
+      for (int q = 0; q < 2 * NPL; ++q) cur[q] = nxt[q];
+    }
+  };
+  // waves g >= G (groups smaller than kFgG) only stage and meet the barriers: their taps
+  // would repeat angle G-1's and burn the LDS bandwidth the real taps are bound by
+  const bool idle = ADMM_FG_EXPT == 1 || (ADMM_FG_IDLE_SKIP && g >= G);
+
+  if constexpr (kDma) {
+    // one 1-KiB piece per wave-instruction: 64 consecutive 16-B slots of one (plane, row,
+    // parity half); a row's even half holds pixels wlo + 2s, its odd half wlo + 2s + 1
+    constexpr int PIECES = NPL * kFgRows * 4;
+    const uint32_t rowbytes = (uint32_t)N * VB * (uint32_t)sizeof(T);
+    auto dma = [&](int m0, int b) {
+      const int rows = min(kFgRows, m_hi - m0);
+      for (int q = g; q < PIECES; q += kFgG) {  // wave-uniform
+        const int h = q & 1, par = (q >> 1) & 1, rp = q >> 2;
+        const int r = rp % kFgRows, pl = rp / kFgRows;
+        if (r >= rows) continue;
+        const int wo = __builtin_amdgcn_readfirstlane(wlo_s[m0 - m_lo + r]);
+        const int wn = __builtin_amdgcn_readfirstlane(wnum_s[m0 - m_lo + r]);
+        if (128 * h + par >= wn) continue;  // piece wholly past the touched width
+        // the row base is block-uniform: force it into SGPRs (a VGPR base makes hipcc wrap
+        // the DMA in a waterfall loop over the distinct resource values)
+        const uint64_t rb = (uint64_t)(uintptr_t)(src + (size_t)(m0 + r) * N * VB);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)rb);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(rb >> 32));
+        const __amdgpu_buffer_rsrc_t rs =
+            make_rsrc((const void*)(uintptr_t)(((uint64_t)hi << 32) | lo), rowbytes);
+        const int col = wo + 128 * h + par + 2 * lane;
+        // negative columns wrap to huge unsigned offsets: out of range, zero-filled
+        const unsigned voff = (unsigned)((col * VB + pl * PV) * (int)sizeof(T));
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void*)&win[b][pl][r][(par ? kFgOdd : 0) + 64 * h], 16, voff,
+            0, 0, 0);
+      }
+    };
+    if (ADMM_FG_EXPT != 2) dma(m_lo, 0);
+    __syncthreads();  // (its fence waits for this wave's LDS-DMA: vmcnt(0)) chunk 0 staged
+    for (int m0 = m_lo, ci = 0; m0 < m_hi; m0 += kFgRows, ++ci) {
+      const int cb = ci & 1;
+      // the other buffer was last read by the previous chunk's taps (done: barrier below)
+      if (ADMM_FG_EXPT != 2 && m0 + kFgRows < m_hi) dma(m0 + kFgRows, cb ^ 1);
+      origins(m0, wl_cur);
+      const int rows = idle ? 0 : min(kFgRows, m_hi - m0);
+      if (ADMM_FG_PIPE && ADMM_FG_EO && rows == kFgRows)
+        taps4(win[cb], m0);
+      else
+        taps(win[cb], m0, rows, wl_cur);
+      __syncthreads();  // this chunk's readers done; next chunk's DMA landed (vmcnt(0) + barrier)
+    }
+  } else {
+    // staging in two halves: issue global loads for chunk c+1 into registers
+    // (prefetch), compute chunk c from LDS, then write the registers into LDS.
+    Pack<T, PV> stage[PER];
+    auto fetch = [&](int m0) {
+      const int rows = min(kFgRows, m_hi - m0);
+#pragma unroll
+      for (int e = 0; e < PER; ++e) {
+        const int q = threadIdx.x + e * kFgThreads;
+        const int pl = q % NPL, rw = q / NPL;
+        const int r = rw / kFgWin, w = rw - r * kFgWin;
+        // only the row's touched width is fetched (the rest of the window is never read)
+        // both reads unconditional (in bounds: +4 padding), so they issue together
+        const int wn = wnum_s[m0 - m_lo + r], wo = wlo_s[m0 - m_lo + r];
+        const int col = (r < rows && w < wn) ? wo + w : -1;
+        if (q < kFgRows * kFgWin * NPL && col >= 0 && col < N) {
+          stage[e] = *reinterpret_cast<const Pack<T, PV>*>(src + ((size_t)(m0 + r) * N + col) * VB + pl * PV);
+        } else {
+#pragma unroll
+          for (int z = 0; z < PV; ++z) stage[e].v[z] = T(0);
+        }
+      }
+    };
+    auto commit = [&]() {
+#pragma unroll
+      for (int e = 0; e < PER; ++e) {
+        const int q = threadIdx.x + e * kFgThreads;
+        if (q < kFgRows * kFgWin * NPL) {
+          const int pl = q % NPL, rw = q / NPL;
+          const int r = rw / kFgWin, w = rw - r * kFgWin;
+          win[0][pl][r][ADMM_FG_EO ? ((w & 1) ? kFgOdd + (w >> 1) : (w >> 1)) : w] = stage[e];
+        }
+      }
+    };
+    if (ADMM_FG_EXPT != 2) fetch(m_lo);
+    for (int m0 = m_lo; m0 < m_hi; m0 += kFgRows) {
+      int wl[kFgRows];
+      origins(m0, wl);
+      __syncthreads();  // previous chunk's readers are done
+      if (ADMM_FG_EXPT != 2) commit();
+      __syncthreads();
+      if (ADMM_FG_PRIO == 1) __builtin_amdgcn_s_setprio(1);
+      if (ADMM_FG_EXPT != 2 && m0 + kFgRows < m_hi) fetch(m0 + kFgRows);
+      if (ADMM_FG_PRIO == 1) __builtin_amdgcn_s_setprio(0);
+      if (ADMM_FG_PRIO == 2) __builtin_amdgcn_s_setprio(1);
+      taps(win[0], m0, idle ? 0 : min(kFgRows, m_hi - m0), wl);
+      if (ADMM_FG_PRIO == 2) __builtin_amdgcn_s_setprio(0);
+    }
   }
   if (g < G && k >= 0 && k < n_det) {
     const size_t m_rays = (size_t)n_ang * n_det;

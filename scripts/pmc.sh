@@ -9,11 +9,12 @@ STEPS=2
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 export ADMM_BENCH_MARKERS=1
 i=0
-for counters in FETCH_SIZE WRITE_SIZE; do
+if [ -n "${PASSFILE:-}" ]; then mapfile -t PASSLIST < "$PASSFILE"; else PASSLIST=("FETCH_SIZE" "WRITE_SIZE"); fi
+for counters in "${PASSLIST[@]}"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $counters --kernel-trace -d gpurun_out/${TAG}_$i -o run --output-format csv -- python bench.py --steps $STEPS --warmup 1 --no-cpu-baseline --strong none > gpurun_out/${TAG}_$i.log 2>&1
   rc=$?
   echo "pass $i ($counters) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/${TAG}_$i.log; exit $rc; fi
 done
-python scripts/traffic_summary.py $TAG $STEPS gpurun_out/${TAG}_traffic.json
+if [ -z "${PASSFILE:-}" ]; then python scripts/traffic_summary.py $TAG $STEPS gpurun_out/${TAG}_traffic.json; fi
