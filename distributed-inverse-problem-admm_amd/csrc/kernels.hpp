@@ -399,6 +399,15 @@ constexpr int kFgSeg = ADMM_FG_SEG;    // row segments (partial sums) per ray
 #ifndef ADMM_FG_PIPE
 #define ADMM_FG_PIPE 1  // software-pipelined taps of full chunks in the LDS-DMA kernel (0: row by row)
 #endif
+#ifndef ADMM_FG_DMA_ROWS
+#define ADMM_FG_DMA_ROWS 2  // rows per chunk of the LDS-DMA kernel (4: 34.7 us, 1: 38.0 us at 512^2 vs 32.5)
+#endif
+#ifndef ADMM_FG_WPAR
+#define ADMM_FG_WPAR 1  // row windows from all G waves with LDS min/max atomics (0: serial loop over angles)
+#endif
+#ifndef ADMM_FG_DMAMASK
+#define ADMM_FG_DMAMASK 0  // 1: LDS-DMA lanes past a row's touched width fetch nothing (+0.7 us: the select costs more than the fetch)
+#endif
 #ifndef ADMM_FG_IDLE_SKIP
 #define ADMM_FG_IDLE_SKIP 1  // waves beyond the group's angle count skip the tap loop (0: tuning A/B)
 #endif
@@ -466,10 +475,47 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   // VGPRs or ds_write instructions spent on staging.  float64 x 8 nodes (4 planes) keeps the
   // register-staged single buffer (two would not fit two blocks per CU).
   constexpr bool kDma = ADMM_FG_DMA && sizeof(Pack<T, PV>) == 16 && NPL <= 2;
-  __shared__ Pack<T, PV> win[kDma ? 2 : 1][NPL][kFgRows][kFgRow];
+  // rows per staged chunk (2 in the LDS-DMA kernel: the next chunk's DMA is issued a
+  // 2-row chunk of taps ahead; 4-row chunks, or a 3/4-buffer ring with counted vmcnt waits
+  // keeping 2-3 chunks in flight, measured slower)
+  constexpr int R = kDma ? ADMM_FG_DMA_ROWS : kFgRows;
+  constexpr int PIECES = NPL * R * 4;  // 1-KiB LDS-DMA pieces per chunk
+  __shared__ Pack<T, PV> win[kDma ? 2 : 1][NPL][R][kFgRow];
   // every row window of the segment (N <= 4096): origin and the width actually touched
   __shared__ __align__(16) int wlo_s[(4096 + kFgSeg - 1) / kFgSeg + 4];  // +4: int4 reads of the last chunk
   __shared__ int wnum_s[(4096 + kFgSeg - 1) / kFgSeg + 4];
+  if constexpr (ADMM_FG_WPAR) {
+    // Row windows in parallel: wave g < G bounds its own angle's rays on every row and
+    // folds floor(l) into the row's min / max with LDS integer atomics (floor is monotone,
+    // so min/max of floors == floor of min/max: the same windows as the serial loop below,
+    // in any order).  The serial form walks the G angles one dependent global load at a
+    // time on 64 threads, exposed at the start of every block.
+    for (int r = threadIdx.x; r < nrows; r += kFgThreads) {
+      wlo_s[r] = INT_MAX;
+      wnum_s[r] = INT_MIN;  // floor(lmax) until the fix-up below
+    }
+    __syncthreads();
+    if (g < G) {  // wave-uniform; a == ang[t0 + g] here
+      const int ka = max(kbase + gr->delta[seg][g], 0), kb = min(kbase + gr->delta[seg][g] + 63, n_det - 1);
+      if (ka <= kb) {
+        const double ca = fma((double)ka, a.A1, a.A0), cb = fma((double)kb, a.A1, a.A0);
+        for (int r = lane; r < nrows; r += 64) {
+          const double dm = (double)(m_lo + r);
+          const double la = fma(dm, a.dl, ca), lb = fma(dm, a.dl, cb);
+          atomicMin(&wlo_s[r], (int)floor(fmin(la, lb)));
+          atomicMax(&wnum_s[r], (int)floor(fmax(la, lb)));
+        }
+      }
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < nrows; r += kFgThreads) {
+      const int fmn = wlo_s[r], fmx = wnum_s[r];
+      const bool any = fmn != INT_MAX;  // always true for host-planned chunks
+      const int wlo = (fmn - 1) & ~1;   // even origin, as below
+      wlo_s[r] = any ? wlo : 0;
+      wnum_s[r] = any ? min(kFgWin, fmx - wlo + 2) : 0;
+    }
+  } else
   for (int r = threadIdx.x; r < nrows; r += kFgThreads) {
     const double dm = (double)(m_lo + r);
     double lmin = 1e300, lmax = -1e300;
@@ -503,11 +549,11 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
 #ifndef ADMM_FG_EXPT
 #define ADMM_FG_EXPT 0  // timing diagnostics only: 1 = no tap loop, 2 = no staging
 #endif
-  int wl_cur[kFgRows];  // the current chunk's window origins (scalars)
+  int wl_cur[R];  // the current chunk's window origins (scalars)
   // the chunk's window origins, read once into scalar registers (a per-row LDS read
   // would put a dependent LDS round trip in front of every row's tap reads)
-  auto origins = [&](int m0, int (&wl)[kFgRows]) {
-    if constexpr (ADMM_FG_W4 && kFgRows == 4) {
+  auto origins = [&](int m0, int (&wl)[R]) {
+    if constexpr (ADMM_FG_W4 && R == 4) {
       const int4 w4 = *reinterpret_cast<const int4*>(&wlo_s[m0 - m_lo]);
       wl[0] = __builtin_amdgcn_readfirstlane(w4.x);
       wl[1] = __builtin_amdgcn_readfirstlane(w4.y);
@@ -515,13 +561,13 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       wl[3] = __builtin_amdgcn_readfirstlane(w4.w);
     } else {
 #pragma unroll
-      for (int r = 0; r < kFgRows; ++r) wl[r] = wlo_s[m0 - m_lo + r];
+      for (int r = 0; r < R; ++r) wl[r] = wlo_s[m0 - m_lo + r];
     }
   };
   // the taps of one staged chunk: every row's two taps per ray from LDS
-  auto taps = [&](const Pack<T, PV> (&wb)[NPL][kFgRows][kFgRow], int m0, int rows, const int (&wl)[kFgRows]) {
+  auto taps = [&](const Pack<T, PV> (&wb)[NPL][R][kFgRow], int m0, int rows, const int (&wl)[R]) {
 #pragma unroll
-    for (int r = 0; r < kFgRows; ++r) {  // unrolled: the chunk's LDS reads can all be in flight
+    for (int r = 0; r < R; ++r) {  // unrolled: the chunk's LDS reads can all be in flight
       if (r >= rows) break;
       int idx;
       T w1;
@@ -567,11 +613,11 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   // then row r+1's LDS reads issued before row r's FMAs, so one row's reads are always in
   // flight behind the other's arithmetic (the LDS-DMA staging freed the registers: the
   // register-staged kernel had no room for the second row's 16).  Same FMAs, same order.
-  auto taps4 = [&](const Pack<T, PV> (&wb)[NPL][kFgRows][kFgRow], int m0) {
-    int se[kFgRows], so[kFgRows];
-    T we[kFgRows], wo[kFgRows];
+  auto taps4 = [&](const Pack<T, PV> (&wb)[NPL][R][kFgRow], int m0) {
+    int se[R], so[R];
+    T we[R], wo[R];
 #pragma unroll
-    for (int r = 0; r < kFgRows; ++r) {
+    for (int r = 0; r < R; ++r) {
       int idx;
       T w1;
       if constexpr (std::is_same<T, float>::value) {
@@ -598,8 +644,8 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       cur[2 * q + 1] = wb[q][0][so[0]];
     }
 #pragma unroll
-    for (int r = 0; r < kFgRows; ++r) {
-      if (r + 1 < kFgRows) {
+    for (int r = 0; r < R; ++r) {
+      if (r + 1 < R) {
 #pragma unroll
         for (int q = 0; q < NPL; ++q) {
           nxt[2 * q] = wb[q][r + 1][se[r + 1]];
@@ -624,13 +670,12 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   if constexpr (kDma) {
     // one 1-KiB piece per wave-instruction: 64 consecutive 16-B slots of one (plane, row,
     // parity half); a row's even half holds pixels wlo + 2s, its odd half wlo + 2s + 1
-    constexpr int PIECES = NPL * kFgRows * 4;
     const uint32_t rowbytes = (uint32_t)N * VB * (uint32_t)sizeof(T);
     auto dma = [&](int m0, int b) {
-      const int rows = min(kFgRows, m_hi - m0);
+      const int rows = min(R, m_hi - m0);
       for (int q = g; q < PIECES; q += kFgG) {  // wave-uniform
         const int h = q & 1, par = (q >> 1) & 1, rp = q >> 2;
-        const int r = rp % kFgRows, pl = rp / kFgRows;
+        const int r = rp % R, pl = rp / R;
         if (r >= rows) continue;
         const int wo = __builtin_amdgcn_readfirstlane(wlo_s[m0 - m_lo + r]);
         const int wn = __builtin_amdgcn_readfirstlane(wnum_s[m0 - m_lo + r]);
@@ -642,9 +687,11 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(rb >> 32));
         const __amdgpu_buffer_rsrc_t rs =
             make_rsrc((const void*)(uintptr_t)(((uint64_t)hi << 32) | lo), rowbytes);
-        const int col = wo + 128 * h + par + 2 * lane;
-        // negative columns wrap to huge unsigned offsets: out of range, zero-filled
-        const unsigned voff = (unsigned)((col * VB + pl * PV) * (int)sizeof(T));
+        const int rel = 128 * h + par + 2 * lane, col = wo + rel;
+        // negative columns wrap to huge unsigned offsets: out of range, zero-filled; so are
+        // slots past the row's touched width (never read by a tap: no L2 fetch spent on them)
+        const unsigned voff = (!ADMM_FG_DMAMASK || rel < wn) ? (unsigned)((col * VB + pl * PV) * (int)sizeof(T))
+                                                             : 0x7ffffff0u;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             rs, (__attribute__((address_space(3))) void*)&win[b][pl][r][(par ? kFgOdd : 0) + 64 * h], 16, voff,
             0, 0, 0);
@@ -652,13 +699,13 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
     };
     if (ADMM_FG_EXPT != 2) dma(m_lo, 0);
     __syncthreads();  // (its fence waits for this wave's LDS-DMA: vmcnt(0)) chunk 0 staged
-    for (int m0 = m_lo, ci = 0; m0 < m_hi; m0 += kFgRows, ++ci) {
+    for (int m0 = m_lo, ci = 0; m0 < m_hi; m0 += R, ++ci) {
       const int cb = ci & 1;
       // the other buffer was last read by the previous chunk's taps (done: barrier below)
-      if (ADMM_FG_EXPT != 2 && m0 + kFgRows < m_hi) dma(m0 + kFgRows, cb ^ 1);
+      if (ADMM_FG_EXPT != 2 && m0 + R < m_hi) dma(m0 + R, cb ^ 1);
       origins(m0, wl_cur);
-      const int rows = idle ? 0 : min(kFgRows, m_hi - m0);
-      if (ADMM_FG_PIPE && ADMM_FG_EO && rows == kFgRows)
+      const int rows = idle ? 0 : min(R, m_hi - m0);
+      if (ADMM_FG_PIPE && ADMM_FG_EO && rows == R)
         taps4(win[cb], m0);
       else
         taps(win[cb], m0, rows, wl_cur);
@@ -669,7 +716,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
     // (prefetch), compute chunk c from LDS, then write the registers into LDS.
     Pack<T, PV> stage[PER];
     auto fetch = [&](int m0) {
-      const int rows = min(kFgRows, m_hi - m0);
+      const int rows = min(R, m_hi - m0);
 #pragma unroll
       for (int e = 0; e < PER; ++e) {
         const int q = threadIdx.x + e * kFgThreads;
@@ -679,7 +726,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         // both reads unconditional (in bounds: +4 padding), so they issue together
         const int wn = wnum_s[m0 - m_lo + r], wo = wlo_s[m0 - m_lo + r];
         const int col = (r < rows && w < wn) ? wo + w : -1;
-        if (q < kFgRows * kFgWin * NPL && col >= 0 && col < N) {
+        if (q < R * kFgWin * NPL && col >= 0 && col < N) {
           stage[e] = *reinterpret_cast<const Pack<T, PV>*>(src + ((size_t)(m0 + r) * N + col) * VB + pl * PV);
         } else {
 #pragma unroll
@@ -691,7 +738,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
 #pragma unroll
       for (int e = 0; e < PER; ++e) {
         const int q = threadIdx.x + e * kFgThreads;
-        if (q < kFgRows * kFgWin * NPL) {
+        if (q < R * kFgWin * NPL) {
           const int pl = q % NPL, rw = q / NPL;
           const int r = rw / kFgWin, w = rw - r * kFgWin;
           win[0][pl][r][ADMM_FG_EO ? ((w & 1) ? kFgOdd + (w >> 1) : (w >> 1)) : w] = stage[e];
@@ -699,17 +746,17 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       }
     };
     if (ADMM_FG_EXPT != 2) fetch(m_lo);
-    for (int m0 = m_lo; m0 < m_hi; m0 += kFgRows) {
-      int wl[kFgRows];
+    for (int m0 = m_lo; m0 < m_hi; m0 += R) {
+      int wl[R];
       origins(m0, wl);
       __syncthreads();  // previous chunk's readers are done
       if (ADMM_FG_EXPT != 2) commit();
       __syncthreads();
       if (ADMM_FG_PRIO == 1) __builtin_amdgcn_s_setprio(1);
-      if (ADMM_FG_EXPT != 2 && m0 + kFgRows < m_hi) fetch(m0 + kFgRows);
+      if (ADMM_FG_EXPT != 2 && m0 + R < m_hi) fetch(m0 + R);
       if (ADMM_FG_PRIO == 1) __builtin_amdgcn_s_setprio(0);
       if (ADMM_FG_PRIO == 2) __builtin_amdgcn_s_setprio(1);
-      taps(win[0], m0, idle ? 0 : min(kFgRows, m_hi - m0), wl);
+      taps(win[0], m0, idle ? 0 : min(R, m_hi - m0), wl);
       if (ADMM_FG_PRIO == 2) __builtin_amdgcn_s_setprio(0);
     }
   }
