@@ -7,5 +7,5 @@ for c in "$@"; do
   rc=$?
   echo "$c rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/config_$c.err; exit $rc; fi
-  python -c "import json; b=json.load(open('gpurun_out/config_$c.json')); print('$c', round(b['value'],2), 'node-updates/s', round(b['ms_per_step'],1), 'ms/step', 'fwd', round(b['roofline']['avg_launch_ms']*1e3,1), 'us frac', round(b['roofline']['frac'],2))"
+  python -c "import json; b=json.load(open('gpurun_out/config_$c.json')); print('$c', round(b['value'],2), 'node-updates/s', round(b['ms_per_step'],1), 'ms/step', 'fwd', round(b['roofline']['avg_launch_ms']*1e3,1), 'us')"
 done
