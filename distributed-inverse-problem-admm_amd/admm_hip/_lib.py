@@ -20,7 +20,7 @@ ADMM_TV_ANISO = 1
 ADMM_FUSE_MIDPOINT = 0
 ADMM_FUSE_WEIGHTED = 1
 ADMM_BATCH_KEEP_X = 1  # admm_batch.flags: x_ext local rows written only by admm_node_update
-ABI_VERSION = 3
+ABI_VERSION = 4
 ADMM_MASK_KNN = 0
 ADMM_MASK_MST = 1
 ADMM_MASK_CHAIN = 2
@@ -93,6 +93,8 @@ SYMBOLS = {
     "admm_abi_version": [],
     "admm_last_error": [],
     "admm_ctx_create": [C.POINTER(C.c_void_p), C.POINTER(Geom), C.c_int, C.c_int, C.c_int],
+    "admm_ctx_create_matrix": [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_longlong, C.c_void_p, C.c_void_p,
+                               C.c_void_p, C.c_int, C.c_int, C.c_int],
     "admm_ctx_destroy": [C.c_void_p],
     "admm_project_fwd": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p],
     "admm_project_adj": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p],

@@ -37,6 +37,7 @@ import torch.distributed as dist
 
 from .exchange import HaloExchange, assemble_stats, gather_images
 from .geometry import RayTransform
+from .matrix import MatrixOperator, as_operators
 from .plan import make_plan
 from .solver import NodeBatch
 
@@ -60,19 +61,18 @@ def eps_target(k: int) -> float:
 def _common_geometry(A_list):
     geoms = set()
     for A in A_list:
-        if not isinstance(A, RayTransform):
+        if not isinstance(A, (RayTransform, MatrixOperator)):
             raise TypeError(
-                "A_dense_list entries must be admm_hip RayTransform operators (matrix-free "
-                f"projector); got {type(A).__name__}.  Dense matrices are not accepted on the "
-                "GPU path -- build operators with block_2_load_odl_data.load_odl_data or "
-                "admm_hip.solver.make_operators.")
+                "A_dense_list entries must be admm_hip operators (RayTransform, MatrixOperator) "
+                f"or matrices; got {type(A).__name__}")
         if A._adjoint:
             raise ValueError("A_dense_list entry is an adjoint view")
         geoms.add((A.geom, A.dtype, A.device))
     if len(geoms) != 1:
         raise NotImplementedError(
-            "all nodes must share one geometry (same angle count): the batched kernels project "
-            "every node with one angle table; choose angles_total divisible by num_nodes")
+            "all nodes must share one operator (same geometry / same matrix): the batched "
+            "kernels project every node with one angle table or one CSR matrix; choose "
+            "angles_total divisible by num_nodes")
     return geoms.pop()
 
 
@@ -101,6 +101,9 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
             raise ValueError("inner_chunks and inner_tol are exclusive")
         tv_iters = inner_chunks[0]
     V_total = len(A_dense_list)
+    # matrices (the reference's dense A_dense_list; dense numpy / torch, scipy.sparse)
+    # become explicit-matrix operators (matrix.py); operators pass through
+    A_dense_list = as_operators(A_dense_list, N=N)
     geom, dtype, device = _common_geometry(A_dense_list)
     if geom.N != N:
         raise ValueError(f"N={N} does not match the operators' N={geom.N}")

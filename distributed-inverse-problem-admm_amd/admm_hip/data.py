@@ -99,9 +99,11 @@ class QProvider:
 
 
 def make_precisions(ops: list[RayTransform], q_mode: str = "arithmetic"):
-    """(Wi_list, Qij_diag) with W from the HIP kernel (block_3_graph_and_precisions.py:11-43)."""
+    """(Wi_list, Qij_diag) with W from the HIP kernel (block_3_graph_and_precisions.py:11-43).
+    ``ops`` may also hold matrices (the reference's dense A_dense_list): matrix.as_operators."""
+    from .matrix import as_operators
     cache, Wi_list, keys = {}, [], []
-    for A in ops:
+    for A in as_operators(ops):
         key = (A.geom, A.dtype, A.device)
         if key not in cache:
             cache[key] = (len(cache), A.column_norms_sq(as_numpy=True))

@@ -81,9 +81,10 @@ def current_stream_handle(device=None) -> int:
 
 
 class _Ctx:
-    """One C context (geometry tables + scratch) per (geometry, dtype, device)."""
+    """One C context (geometry tables + scratch) per (geometry, dtype, device); the
+    geometry may also be an explicit matrix (matrix.MatrixGeometry)."""
 
-    def __init__(self, geom: ParallelBeamGeometry, dtype: str, device: int, max_images: int = 64):
+    def __init__(self, geom, dtype: str, device: int, max_images: int = 64):
         self.lib = _lib.load()
         # the library keeps 32-bit element offsets per batch: cap the image count so
         # max_images x max(n, m) x 8 bytes stays below 2^31 (apply() splits larger batches)
@@ -91,11 +92,14 @@ class _Ctx:
         self.geom = geom
         self.dtype = dtype
         self.device = device
-        h = C.c_void_p()
-        g = geom.to_c()
-        code = _lib.ADMM_DTYPE_F64 if dtype == "float64" else _lib.ADMM_DTYPE_F32
-        _lib.check(self.lib.admm_ctx_create(C.byref(h), C.byref(g), code, max_images, device),
-                   "admm_ctx_create")
+        if hasattr(geom, "create_ctx"):  # explicit matrix (matrix.MatrixGeometry)
+            h = geom.create_ctx(self.lib, dtype, device, max_images)
+        else:
+            h = C.c_void_p()
+            g = geom.to_c()
+            code = _lib.ADMM_DTYPE_F64 if dtype == "float64" else _lib.ADMM_DTYPE_F32
+            _lib.check(self.lib.admm_ctx_create(C.byref(h), C.byref(g), code, max_images, device),
+                       "admm_ctx_create")
         self.h = h
         self.max_images = max_images
 

@@ -6,10 +6,12 @@
   masks from one HIP launch (admm_hip.masks) and the masked Q_ij provider.
 
 Deviation: the reference loads a pickled list of dense matrices from
-``base_dir/A_dense_list_pickle`` (:289-295).  Dense A is infeasible past ~128^2
-and unpickling is not done here: pass ``ops=`` (the RayTransform list of
-``load_odl_data``) or ``Wi_list=`` instead.  ``keep`` comes back as a device
-uint8 tensor [V, V, n] (the reference returns a numpy bool array).
+``base_dir/A_dense_list_pickle`` (:289-295).  Pickles are not unpickled here: the
+list is read from ``.npy`` / ``.npz`` files (``admm_hip.matrix.load_matrix_list``,
+allow_pickle=False) when ``A_dense_list_pickle`` names one, else pass ``ops=`` (the
+RayTransform list of ``load_odl_data``, or matrices) or ``Wi_list=``.  Dense A is
+infeasible past ~128^2.  ``keep`` comes back as a device uint8 tensor [V, V, n]
+(the reference returns a numpy bool array).
 """
 from __future__ import annotations
 
@@ -30,9 +32,14 @@ def build_pixel_connected_Q_provider(base_dir="saved_operators_Incmp_Span",
     """Returns (G_union, Wi_list, Qij_diag_masked, keep) like block_3:265-319."""
     if Wi_list is None:
         if ops is None:
-            raise FileNotFoundError(
-                f"no operators given: the reference reads {os.path.join(base_dir, A_dense_list_pickle)} "
-                "(pickled dense matrices); pass ops=<RayTransform list> or Wi_list= instead")
+            path = os.path.join(base_dir, A_dense_list_pickle)
+            if os.path.splitext(path)[1].lower() in (".npy", ".npz") and os.path.exists(path):
+                from admm_hip.matrix import as_operators, load_matrix_list
+                ops = as_operators(load_matrix_list(path), device=device)
+            else:
+                raise FileNotFoundError(
+                    f"no operators given: the reference reads {path} (pickled dense matrices, "
+                    "not unpickled here); save the list as .npy / .npz, or pass ops= or Wi_list=")
         Wi_list, _ = make_precisions(ops, q_mode=q_mode)
     if device is None:
         from admm_hip.geometry import default_device

@@ -28,6 +28,7 @@ import torch
 from admm_hip import _lib
 from admm_hip.admm import DEFAULT_MU_FACTOR
 from admm_hip.geometry import RayTransform
+from admm_hip.matrix import MatrixOperator, as_operators
 from admm_hip.plan import ShardPlan
 from admm_hip.solver import NodeBatch
 
@@ -58,9 +59,10 @@ def _star_plan(deg: int) -> ShardPlan:
 
 class _Problem:
     def __init__(self, Ai, bi, rho, neighbor_terms, N, lam_tv, Qij_terms, xi):
-        if not isinstance(Ai, RayTransform) or Ai._adjoint:
-            raise TypeError("Ai must be an admm_hip RayTransform (matrix-free projector), got "
-                            f"{type(Ai).__name__}")
+        if not isinstance(Ai, (RayTransform, MatrixOperator)):
+            Ai = as_operators([Ai], N=N)[0]  # a matrix (dense / scipy.sparse): explicit-matrix operator
+        if Ai._adjoint:
+            raise TypeError("Ai is an adjoint view")
         if Ai.geom.N != N:
             raise ValueError(f"N={N} does not match the operator's N={Ai.geom.N}")
         if len(neighbor_terms) != len(Qij_terms):

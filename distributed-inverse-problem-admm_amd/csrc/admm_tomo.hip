@@ -85,6 +85,12 @@ struct admm_ctx {
   int fg_nblk = 0, fg_order_nch = 0;
   hipStream_t cap = nullptr;  // private capture stream
 
+  // explicit-matrix context (admm_ctx_create_matrix): A and A^T as device CSR, values in
+  // the sample dtype; the projector launches dispatch to k_csr_fwd / k_back<..., CSR>
+  bool csr = false;
+  long long nnz = 0;
+  Buf f_ptr, f_idx, f_val, t_ptr, t_idx, t_val;
+
   // operator-API scratch (admm_project_fwd runs the hot grouped kernel on up to 8 images
   // per launch: node-major images packed into the interleaved sample layout)
   Buf op_img, op_imgT, op_sino, op_fpart;
@@ -237,6 +243,13 @@ int with_vb(int vb, F&& f) {
 
 template <typename T, int VB, int MODE>
 int launch_fwd(admm_ctx* C, const T* img, const T* imgT, T* sino, const T* b, double* part, int V, hipStream_t s) {
+  if (C->csr) {  // explicit matrix: one thread per sinogram row
+    dim3 cg((C->mrays + kBlock - 1) / kBlock, (V + VB - 1) / VB);
+    hipLaunchKernelGGL((k_csr_fwd<T, VB, MODE>), cg, dim3(kBlock), 0, s, (const int*)C->f_ptr.p,
+                       (const int*)C->f_idx.p, (const T*)C->f_val.p, img, sino, b, part, C->mrays, C->npix, V);
+    CHECK_LAUNCH();
+    return ADMM_OK;
+  }
   dim3 grid((C->g.n_det + kFwdRays - 1) / kFwdRays, C->g.n_angles, (V + VB - 1) / VB);
   hipLaunchKernelGGL((k_fwd<T, VB, MODE>), grid, dim3(kFwdBlock), 0, s, img, imgT, sino, b, part, C->fang, C->g.N,
                      C->g.n_det, C->g.n_angles, V);
@@ -287,7 +300,14 @@ int launch_back(admm_ctx* C, BackArgs<T> a, int V, hipStream_t s) {
   a.V = V;
   const int N = C->g.N;
   dim3 grid((N + kBTJ - 1) / kBTJ, (N + kBTI - 1) / kBTI, MODE == BACK_WSQ ? 1 : (V + VB - 1) / VB);
-  hipLaunchKernelGGL((k_back<T, VB, MODE>), grid, dim3(kBkThreads), 0, s, a);
+  if (C->csr) {
+    a.csr_ptr = (const int*)C->t_ptr.p;
+    a.csr_idx = (const int*)C->t_idx.p;
+    a.csr_val = (const T*)C->t_val.p;
+    hipLaunchKernelGGL((k_back<T, VB, MODE, true>), grid, dim3(kBkThreads), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((k_back<T, VB, MODE>), grid, dim3(kBkThreads), 0, s, a);
+  }
   CHECK_LAUNCH();
   return ADMM_OK;
 }
@@ -531,6 +551,7 @@ template <typename T>
 int op_forward(admm_ctx* C, const T* img, T* sino, int nimg, hipStream_t s) {
   const size_t npix = C->npix, m = C->mrays, ds = sizeof(T);
   const int N = C->g.N;
+  if (C->csr) return launch_fwd<T, 1, 0>(C, img, nullptr, sino, nullptr, nullptr, nimg, s);
   if (C->plan_n[0] == 0) {  // no angle-group plan for this geometry: ray-per-thread kernel
     RET(ensure(C->op_imgT, (size_t)nimg * npix * ds));
     hipLaunchKernelGGL((k_transpose<T, 1>), tile_grid(C, nimg, 1), dim3(kBlock), 0, s, img, (T*)C->op_imgT.p, N);
@@ -721,13 +742,104 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
   return ADMM_OK;
 }
 
+int admm_ctx_create_matrix(admm_ctx** out, int N, int m, long long nnz, const long long* indptr,
+                           const int* indices, const double* values, int dtype, int max_images, int device) {
+  if (!out || !indptr || (nnz > 0 && (!indices || !values))) return fail(ADMM_E_INVALID, "null argument");
+  *out = nullptr;
+  if (N < 2 || N > 4096 || m < 1) return fail(ADMM_E_INVALID, "bad matrix sizes");
+  if (dtype != ADMM_DTYPE_F32 && dtype != ADMM_DTYPE_F64) return fail(ADMM_E_INVALID, "bad dtype");
+  if (max_images < 1) return fail(ADMM_E_INVALID, "max_images < 1");
+  const size_t npix = (size_t)N * N;
+  if (nnz < 0 || nnz >= (1ll << 31)) return fail(ADMM_E_INVALID, "nnz must be < 2^31");
+  if ((size_t)max_images * npix * 8 >= (1ull << 31) || (size_t)max_images * m * 8 >= (1ull << 31))
+    return fail(ADMM_E_INVALID, "batch too large for 32-bit buffer offsets; split it across contexts");
+  if (indptr[0] != 0 || indptr[m] != nnz) return fail(ADMM_E_INVALID, "indptr must run from 0 to nnz");
+  for (int r = 0; r < m; ++r)
+    if (indptr[r + 1] < indptr[r]) return fail(ADMM_E_INVALID, "indptr not non-decreasing");
+  for (long long k = 0; k < nnz; ++k)
+    if (indices[k] < 0 || (size_t)indices[k] >= npix) return fail(ADMM_E_INVALID, "column index out of range");
+  // A^T by a counting sort over columns; within a column the rows stay ascending
+  std::vector<int> tptr(npix + 1, 0), tidx((size_t)nnz);
+  std::vector<double> tval((size_t)nnz);
+  for (long long k = 0; k < nnz; ++k) ++tptr[(size_t)indices[k] + 1];
+  for (size_t c = 0; c < npix; ++c) tptr[c + 1] += tptr[c];
+  {
+    std::vector<int> fill(tptr.begin(), tptr.end() - 1);
+    for (int r = 0; r < m; ++r)
+      for (long long k = indptr[r]; k < indptr[r + 1]; ++k) {
+        const int q = fill[indices[k]]++;
+        tidx[q] = r;
+        tval[q] = values[k];
+      }
+  }
+  std::vector<int> fptr(m + 1);
+  for (int r = 0; r <= m; ++r) fptr[r] = (int)indptr[r];
+  HIPCHK(hipSetDevice(device));
+  admm_ctx* C = new admm_ctx();
+  // a one-"angle" geometry (n_det = m, L = 1): every m-sized buffer, the fixed-order
+  // reductions and the combine/residual kernels keep their shapes
+  C->g = admm_geom{};
+  C->g.N = N;
+  C->g.n_angles = 1;
+  C->g.n_det = m;
+  C->dtype = dtype;
+  C->device = device;
+  C->max_images = max_images;
+  C->npix = (int)npix;
+  C->mrays = m;
+  C->csr = true;
+  C->nnz = nnz;
+  const char* ng = getenv("ADMM_NO_GRAPH");
+  C->use_graph = !(ng && ng[0] == '1');
+  FwdAngle fa{};
+  fa.L = 1.0;
+  BackAngle ba{};
+  BackAngleC bc{};
+  int rc = ADMM_OK;
+  auto up = [&](Buf& b, const void* src, size_t bytes) {
+    if (rc != ADMM_OK) return;
+    rc = ensure(b, std::max<size_t>(bytes, 16));
+    if (rc == ADMM_OK && bytes > 0 && hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice) != hipSuccess)
+      rc = fail(ADMM_E_HIP, "hipMemcpy (matrix upload)");
+  };
+  auto upv = [&](Buf& b, const std::vector<double>& v) {
+    if (dtype == ADMM_DTYPE_F64) return up(b, v.data(), v.size() * 8);
+    std::vector<float> f(v.begin(), v.end());
+    up(b, f.data(), f.size() * 4);
+  };
+  up(C->f_ptr, fptr.data(), fptr.size() * 4);
+  up(C->f_idx, indices, (size_t)nnz * 4);
+  upv(C->f_val, std::vector<double>(values, values + nnz));
+  up(C->t_ptr, tptr.data(), tptr.size() * 4);
+  up(C->t_idx, tidx.data(), tidx.size() * 4);
+  upv(C->t_val, tval);
+  if (rc == ADMM_OK && (hipMalloc(&C->fang, sizeof(FwdAngle)) != hipSuccess ||
+                        hipMalloc(&C->bang, sizeof(BackAngle)) != hipSuccess ||
+                        hipMalloc(&C->bangc, sizeof(BackAngleC)) != hipSuccess))
+    rc = fail(ADMM_E_HIP, "hipMalloc tables");
+  if (rc == ADMM_OK && (hipMemcpy(C->fang, &fa, sizeof(fa), hipMemcpyHostToDevice) != hipSuccess ||
+                        hipMemcpy(C->bang, &ba, sizeof(ba), hipMemcpyHostToDevice) != hipSuccess ||
+                        hipMemcpy(C->bangc, &bc, sizeof(bc), hipMemcpyHostToDevice) != hipSuccess))
+    rc = fail(ADMM_E_HIP, "hipMemcpy tables");
+  if (rc == ADMM_OK && hipStreamCreateWithFlags(&C->cap, hipStreamNonBlocking) != hipSuccess)
+    rc = fail(ADMM_E_HIP, "hipStreamCreate");
+  if (rc != ADMM_OK) {
+    const std::string msg = g_err;
+    admm_ctx_destroy(C);
+    return fail(rc, msg);
+  }
+  *out = C;
+  return ADMM_OK;
+}
+
 int admm_ctx_destroy(admm_ctx* C) {
   if (!C) return ADMM_OK;
   (void)hipSetDevice(C->device);
   (void)hipDeviceSynchronize();
   free_graphs(C);
   Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->op_sino, &C->op_fpart, &C->op_order[0], &C->op_order[1], &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->bI, &C->fpart, &C->r, &C->c,
-                 &C->d2, &C->e2, &C->partH, &C->partS, &C->partD, &C->partE, &C->redH, &C->fg_order, &C->dsumS, &C->ats};
+                 &C->d2, &C->e2, &C->partH, &C->partS, &C->partD, &C->partE, &C->redH, &C->fg_order, &C->dsumS, &C->ats,
+                 &C->f_ptr, &C->f_idx, &C->f_val, &C->t_ptr, &C->t_idx, &C->t_val};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (C->fang) (void)hipFree(C->fang);
@@ -849,8 +961,8 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   C->P_tile = ((N + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
   if ((size_t)Vp * npix * ds >= (1ull << 31) || (size_t)Vp * m * ds >= (1ull << 31))
     return fail(ADMM_E_INVALID, "batch too large for 32-bit buffer offsets");
-  C->P_fwd = C->n_groups > 0 ? (int)((m + kBlock - 1) / kBlock)
-                             : ((C->g.n_det + kFwdRays - 1) / kFwdRays) * C->g.n_angles;
+  C->P_fwd = (C->n_groups > 0 || C->csr) ? (int)((m + kBlock - 1) / kBlock)
+                                         : ((C->g.n_det + kFwdRays - 1) / kFwdRays) * C->g.n_angles;
   C->P_edge = (int)((npix + kBlock * 4 - 1) / (kBlock * 4));
   RET(ensure(C->partH, (size_t)5 * V * C->P_back * 8));
   RET(ensure(C->partS, (size_t)V * C->P_fwd * 8));

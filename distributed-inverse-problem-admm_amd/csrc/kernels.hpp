@@ -349,6 +349,59 @@ __global__ __launch_bounds__(kFwdBlock) void k_fwd(const T* __restrict__ img, co
 }
 
 // ===========================================================================
+// Explicit-matrix forward (admm_ctx_create_matrix): sino = A x with A a CSR matrix
+// (rows = sinogram entries in the reference's angle-major order, columns = C-order
+// pixels), for operators given as matrices (the reference's A_dense_list,
+// block_2_load_odl_data.py:68-96 / block_7_main.py:16-22) instead of a geometry.
+// One thread per row over VB interleaved nodes; same outputs as k_fwd (MODE 0 / 1),
+// ||s||^2 partials per 256-row block.
+// ===========================================================================
+template <typename T, int VB, int MODE>
+__global__ __launch_bounds__(kBlock) void k_csr_fwd(const int* __restrict__ ptr, const int* __restrict__ idx,
+                                                    const T* __restrict__ val, const T* __restrict__ img,
+                                                    T* __restrict__ sino, const T* __restrict__ bsino,
+                                                    double* __restrict__ part, int m, int npix, int V) {
+  const int chunk = blockIdx.y, v0 = chunk * VB, nv = min(VB, V - v0);
+  const int row = blockIdx.x * kBlock + threadIdx.x;
+  const T* src = img + (size_t)chunk * npix * VB;
+  double sq[VB];
+#pragma unroll
+  for (int u = 0; u < VB; ++u) sq[u] = 0.0;
+  if (row < m) {
+    T acc[VB], pv[VB];
+#pragma unroll
+    for (int u = 0; u < VB; ++u) acc[u] = T(0);
+    for (int k = ptr[row]; k < ptr[row + 1]; ++k) {
+      const T w = val[k];
+      gload<T, VB>(src + (size_t)idx[k] * VB, pv);
+#pragma unroll
+      for (int u = 0; u < VB; ++u) acc[u] = fma(w, pv[u], acc[u]);
+    }
+    if (MODE == 1) {
+#pragma unroll
+      for (int u = 0; u < VB; ++u) {
+        if (u < nv) {
+          acc[u] = acc[u] - bsino[(size_t)(v0 + u) * m + row];
+          sq[u] = (double)acc[u] * (double)acc[u];
+        } else {
+          acc[u] = T(0);
+        }
+      }
+    }
+    gstore<T, VB>(sino + ((size_t)chunk * m + row) * VB, acc);
+  }
+  if (MODE == 1) {
+    __shared__ double lds[4 * VB];
+    block_reduce<VB>(sq, lds);
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int u = 0; u < VB; ++u)
+        if (u < nv) part[(size_t)(v0 + u) * gridDim.x + blockIdx.x] = sq[u];
+    }
+  }
+}
+
+// ===========================================================================
 // Forward projector, angle-grouped (the hot-path version).
 // Block = G <= 4 consecutive angles of one case (one wave each) x 64 consecutive
 // detector bins, over one of kFgSeg row segments.  Rows are processed in chunks of
@@ -839,6 +892,10 @@ struct BackArgs {
   const BackAngleC* angc;   // [n_ang] compact records
   double K;                 // angle-independent part of k_f
   int N, n_det, n_ang, V;
+  // explicit-matrix contexts (admm_ctx_create_matrix): A^T as CSR, one row per pixel
+  const int* csr_ptr;       // [n + 1]
+  const int* csr_idx;       // [nnz] sinogram rows (rays)
+  const T* csr_val;         // [nnz]
   // outputs
   T* out_t;                 // PLAIN: A^T s;  H: Hp;  INIT: p   (interleaved)
   double* out_d;            // ATB: atb;  WSQ: W;  INIT: r     (float64 node-major)
@@ -1120,7 +1177,7 @@ __device__ __forceinline__ void diag_epilogue_tile(const BackArgs<T>& A, double*
   }
 }
 
-template <typename T, int VB, int MODE>
+template <typename T, int VB, int MODE, bool CSR = false>
 __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
   constexpr int NQ = (MODE == BACK_H) ? 5 : (MODE == BACK_DIAG) ? 5 : 1;
   constexpr int NPL = Planes<T, VB>::NPL, PV = Planes<T, VB>::PV;
@@ -1239,7 +1296,24 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
       if (a < nt) win[pl][a][w] = wst[e];
     }
   };
-  if constexpr (PF) {
+  if constexpr (CSR) {
+    // explicit matrix: this pixel's row of A^T (same tile / epilogue as the projector)
+    if (inb) {
+      const int pix = i * N + j;
+      Pack<T, VB> sv;
+      for (int k = A.csr_ptr[pix]; k < A.csr_ptr[pix + 1]; ++k) {
+        const T w = A.csr_val[k];
+        if constexpr (MODE == BACK_WSQ) {
+          acc[0] = fma(w, w, acc[0]);
+        } else {
+          sv = *reinterpret_cast<const Pack<T, VB>*>(sino_c + (size_t)A.csr_idx[k] * VB);
+#pragma unroll
+          for (int u = 0; u < VB; ++u) acc[u] = fma(w, sv.v[u], acc[u]);
+        }
+      }
+    }
+  }
+  if constexpr (PF && !CSR) {
     kmin_chunk(0, 0);
     __syncthreads();
     wfetch(0, 0);
@@ -1247,7 +1321,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
     if (ANGC < n_ang) kmin_chunk(ANGC, 1);
     __syncthreads();
   }
-  for (int t0 = 0, ci = 0; t0 < n_ang; t0 += ANGC, ++ci) {
+  for (int t0 = 0, ci = 0; !CSR && t0 < n_ang; t0 += ANGC, ++ci) {
     const int nt = min(ANGC, n_ang - t0);
     const int kb = (PF) ? (ci & 1) : 0;  // kmin buffer of this chunk
     if constexpr (PF) {

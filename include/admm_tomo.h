@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ADMM_ABI_VERSION 3
+#define ADMM_ABI_VERSION 4
 
 #define ADMM_OK 0
 #define ADMM_E_INVALID (-1)
@@ -143,6 +143,16 @@ const char* admm_last_error(void);
 /* Context: geometry tables + scratch.  dtype = ADMM_DTYPE_*.  max_images bounds
  * the batch size of the operator entry points below. */
 int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_images, int device);
+/* ABI 4: a context for an operator given as an explicit matrix instead of a geometry:
+ * the reference's A_dense_list entries (block_2_load_odl_data.py:68-96 `_to_dense_matrix`,
+ * loaded back at block_7_main.py:16-22 / block_3_graph_and_precisions.py:283-287).
+ * HOST arrays: A (m x N*N, rows = sinogram entries in the layout above, columns = C-order
+ * pixels) as CSR -- indptr[m + 1] (int64), indices[nnz] (int32), values[nnz] (float64,
+ * rounded to the context dtype).  The library keeps A and A^T as device CSR; every entry
+ * point below (operator, batch, consensus) works unchanged, with the projector replaced
+ * by CSR products.  nnz < 2^31. */
+int admm_ctx_create_matrix(admm_ctx** out, int N, int m, long long nnz, const long long* indptr,
+                           const int* indices, const double* values, int dtype, int max_images, int device);
 int admm_ctx_destroy(admm_ctx* ctx);
 
 /* --- operator entry points (replace ODL RayTransform / dense A) ---------- */

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
         assert name in _lib.SYMBOLS, f"{name} not bound in _lib.SYMBOLS"
     assert set(_lib.SYMBOLS) == set(names)
-    assert lib.admm_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.admm_abi_version() == _lib.ABI_VERSION == 4
 
 
 def test_error_path_without_gpu_work():
@@ -126,12 +126,17 @@ def test_history_keys_match_reference():
                                  "eps_target_history"}
 
 
-def test_dense_matrix_is_rejected_loudly():
+def test_non_operator_is_rejected_loudly():
+    """Matrices are accepted (explicit-matrix operators, admm_hip/matrix.py); anything that is
+    neither an operator nor a 2-D matrix fails before any GPU work."""
     import numpy as np
     import networkx as nx
     from block_6_admm_loop_ver2 import decentralized_admm
-    with pytest.raises(TypeError, match="RayTransform"):
-        decentralized_admm([np.zeros((4, 4))], [np.zeros(4)], nx.path_graph(1), [np.ones(4)],
+    with pytest.raises(ValueError, match="2-D"):
+        decentralized_admm([np.zeros(4)], [np.zeros(4)], nx.path_graph(1), [np.ones(4)],
+                           lambda i, j: np.ones(4), 2)
+    with pytest.raises(ValueError, match="N\\*N"):
+        decentralized_admm([np.zeros((4, 5))], [np.zeros(4)], nx.path_graph(1), [np.ones(4)],
                            lambda i, j: np.ones(4), 2)
 
 
