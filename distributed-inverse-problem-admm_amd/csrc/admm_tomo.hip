@@ -103,6 +103,7 @@ struct admm_ctx {
   int vb = 1;  // node interleave width of the sample buffers
   Buf xs, xsT, p, pT, Hp, sino, bI, fpart, r, c, d2, e2;
   Buf dsumS;  // D = sum_j q_ij as interleaved samples (BACK_H epilogue)
+  Buf x2, p2; // ping-pong partners of x (local rows) and p for the fused TV update (ADMM_TV_FUSE)
   Buf ats;    // A^T (A xs - b) of the last update's final x (ADMM_BATCH_KEEP_X)
   bool ats_valid = false;  // ats matches x_ext's local rows
   hipGraph_t g_update_reuse = nullptr;
@@ -394,6 +395,11 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 
   double* ecur = B.e;
   double* dnxt = (double*)C->d2.p;
   double* enxt = (double*)C->e2.p;
+  // ADMM_TV_FUSE: the round's last CG step runs inside the TV update, which reads x and p
+  // over its tiles' halos while writing them: x and p ping-pong (xcur -> xnxt, p -> pnxt)
+  double* xcur = B.x_ext;
+  double* xnxt = (double*)C->x2.p;
+  T* pnxt = (T*)C->p2.p;
   const int K = B.cg_iters, Tt = rounds > 0 ? rounds : B.tv_iters;
   for (int t = 0; t < Tt; ++t) {
     for (int kk = 0; kk < K; ++kk) {
@@ -411,25 +417,34 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 
       a.mu = B.mu;
       RET((launch_back<T, VB, BACK_H>(C, a, V, s)));
       RET(launch_reduce((double*)C->partH.p, 5 * V, Pb, redH, 1, 1, 0, s));
-      if (kk + 1 < K || !ADMM_CG_SKIP_P)
-        hipLaunchKernelGGL((k_cg_update<T, VB, true>), cgg, dim3(kBlock), 0, s, B.x_ext, r, p, pT, Hp, redH, N, V);
-      else  // p is overwritten next (TV update / next x-update start)
-        hipLaunchKernelGGL((k_cg_update<T, VB, false>), cgg, dim3(kBlock), 0, s, B.x_ext, r, p, pT, Hp, redH, N, V);
-      CHECK_LAUNCH();
+      if (kk + 1 < K || !ADMM_CG_SKIP_P) {
+        hipLaunchKernelGGL((k_cg_update<T, VB, true>), cgg, dim3(kBlock), 0, s, xcur, r, p, pT, Hp, redH, N, V);
+        CHECK_LAUNCH();
+      } else if (!ADMM_TV_FUSE) {  // p is overwritten next (TV update / next x-update start)
+        hipLaunchKernelGGL((k_cg_update<T, VB, false>), cgg, dim3(kBlock), 0, s, xcur, r, p, pT, Hp, redH, N, V);
+        CHECK_LAUNCH();
+      }
     }
     const bool last = (t + 1 == Tt);
+    constexpr bool F = ADMM_TV_FUSE && ADMM_CG_SKIP_P;
     if (!last) {
-      hipLaunchKernelGGL((k_tv_update<T, VB, false>), tg, dim3(kBlock), 0, s, B.x_ext, dcur, ecur, dnxt, enxt, r,
-                         p, pT, tau, B.mu, B.tv_kind, N, V);
+      hipLaunchKernelGGL((k_tv_update<T, VB, false, F>), tg, dim3(kBlock), 0, s, xcur, dcur, ecur, dnxt, enxt, r,
+                         F ? pnxt : p, pT, tau, B.mu, B.tv_kind, N, V, xnxt, p, Hp, redH);
       CHECK_LAUNCH();
     } else {
-      hipLaunchKernelGGL((k_tv_update<T, VB, true>), tg, dim3(kBlock), 0, s, B.x_ext, dcur, ecur, dnxt, enxt, r,
-                         xs, xsT, tau, B.mu, B.tv_kind, N, V);
+      hipLaunchKernelGGL((k_tv_update<T, VB, true, F>), tg, dim3(kBlock), 0, s, xcur, dcur, ecur, dnxt, enxt, r,
+                         xs, xsT, tau, B.mu, B.tv_kind, N, V, xnxt, p, Hp, redH);
       CHECK_LAUNCH();
     }
     std::swap(dcur, dnxt);
     std::swap(ecur, enxt);
+    if (F) {
+      std::swap(xcur, xnxt);
+      if (!last) std::swap(p, pnxt);
+    }
   }
+  if (xcur != B.x_ext)  // odd number of fused rounds: x ended in scratch
+    HIPCHK(hipMemcpyAsync(B.x_ext, xcur, (size_t)V * npix * sizeof(double), hipMemcpyDeviceToDevice, s));
   if (dcur != B.d) {  // odd number of rounds: state ended in scratch
     HIPCHK(hipMemcpyAsync(B.d, dcur, 2 * V * npix * sizeof(double), hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(B.e, ecur, 2 * V * npix * sizeof(double), hipMemcpyDeviceToDevice, s));
@@ -839,7 +854,7 @@ int admm_ctx_destroy(admm_ctx* C) {
   free_graphs(C);
   Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->op_sino, &C->op_fpart, &C->op_order[0], &C->op_order[1], &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->bI, &C->fpart, &C->r, &C->c,
                  &C->d2, &C->e2, &C->partH, &C->partS, &C->partD, &C->partE, &C->redH, &C->fg_order, &C->dsumS, &C->ats,
-                 &C->f_ptr, &C->f_idx, &C->f_val, &C->t_ptr, &C->t_idx, &C->t_val};
+                 &C->f_ptr, &C->f_idx, &C->f_val, &C->t_ptr, &C->t_idx, &C->t_val, &C->x2, &C->p2};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (C->fang) (void)hipFree(C->fang);
@@ -947,6 +962,10 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   RET(ensure(C->pT, Vp * npix * ds));
   RET(ensure(C->Hp, Vp * npix * ds));
   RET(ensure(C->dsumS, Vp * npix * ds));
+  if (ADMM_TV_FUSE) {
+    RET(ensure(C->x2, (size_t)V * npix * 8));
+    RET(ensure(C->p2, Vp * npix * ds));
+  }
   if (B.flags & ADMM_BATCH_KEEP_X) RET(ensure(C->ats, Vp * npix * ds));
   C->ats_valid = false;
   RET(ensure(C->sino, Vp * m * ds));

@@ -1577,6 +1577,9 @@ __global__ __launch_bounds__(kBlock) void k_transpose(const T* __restrict__ in, 
 // runs (a node-per-lane mapping splits those into 64-B pieces across 8 arrays 2 MB apart).
 constexpr int kCgRows = kBlock / kTile;  // 8 rows x 32 columns per block
 
+#ifndef ADMM_TV_FUSE
+#define ADMM_TV_FUSE 1  // the round's last CG step fused into the TV update (0: separate kernels)
+#endif
 #ifndef ADMM_CG_SKIP_P
 #define ADMM_CG_SKIP_P 1  // 0: every CG step writes p (A/B timing only)
 #endif
@@ -1622,8 +1625,8 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(double* __restrict__ x, do
         const size_t o = (size_t)(v0 + u) * npix + pix;
         const double alpha = ab_s[u][0], beta = ab_s[u][1];
         const double pd = (double)pv[u];
-        x[o] += alpha * pd;
-        const double rn = r[o] - alpha * (double)hv[u];
+        x[o] = fma(alpha, pd, x[o]);  // (explicit fma: k_tv_update<FUSE> repeats it bitwise)
+        const double rn = fma(-alpha, (double)hv[u], r[o]);
         r[o] = rn;
         np[u] = (T)(rn + beta * pd);
       }
@@ -1668,12 +1671,20 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
-template <typename T, int VB, bool LAST>
+// FUSE: the round's last CG step (k_cg_update<..., false>: x += alpha p, r -= alpha Hp) is
+// folded in.  x after that step is formed wherever the stencil reads it (tile + halo) from
+// the old x and p (pcg) with the same fma, written once to xout (x ping-pongs: neighbour
+// blocks still read the old x), and r gets both updates in one pass; the CG restart p = r
+// goes to a buffer other than pcg for the same reason.  Bitwise the same as the two
+// kernels; saves the CG update's x / r round trip through HBM and one launch per round.
+template <typename T, int VB, bool LAST, bool FUSE = false>
 __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__ x, const double* __restrict__ din,
                                                       const double* __restrict__ ein, double* __restrict__ dout,
                                                       double* __restrict__ eout, double* __restrict__ r,
                                                       T* __restrict__ p, T* __restrict__ pT, double tau,
-                                                      double mu, int kind, int N, int V) {
+                                                      double mu, int kind, int N, int V, double* __restrict__ xout,
+                                                      const T* __restrict__ pcg, const T* __restrict__ Hp,
+                                                      const double* __restrict__ redH) {
   __shared__ TileT<T, VB> tl;
   const EwMap<VB> mp;
   const int chunk = blockIdx.z, v = chunk * VB + mp.u;
@@ -1682,9 +1693,50 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
   const size_t sbase = (size_t)chunk * npix * VB;
   const int wg = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
   const int i0 = (wg / gridDim.x) * EwMap<VB>::TI, j0 = (wg % gridDim.x) * kTile;
+  __shared__ double al_s[VB];
+  if constexpr (FUSE) {  // alpha of the round's last CG step (as k_cg_update)
+    if ((int)threadIdx.x < VB) {
+      const int vv = chunk * VB + threadIdx.x;
+      double alpha = 0.0;
+      if (vv < V) {
+        const double pHp = redH[5 * vv], rp = redH[5 * vv + 4];
+        alpha = (pHp != 0.0) ? rp / pHp : 0.0;
+      }
+      al_s[threadIdx.x] = alpha;
+    }
+    __syncthreads();
+  }
+  // FUSE: p over the block's stencil region (rows i0-1 .. i0+TI, columns j0-1 .. j0+kTile),
+  // staged node-major in LDS with one 32-B vector load per pixel (read per node straight from
+  // the interleaved samples, the stencil's loads were 4 B every 32 B: 65 vs 55 us)
+  constexpr int PR = EwMap<VB>::TI + 2, PC = kTile + 2;
+  __shared__ T p_s[FUSE ? VB : 1][FUSE ? PR : 1][FUSE ? PC + 1 : 1];
+  if constexpr (FUSE) {
+    for (int q = threadIdx.x; q < PR * PC; q += kBlock) {
+      const int rr = q / PC, cc = q % PC;
+      const int i = i0 - 1 + rr, j = j0 - 1 + cc;
+      T pv[VB];
+#pragma unroll
+      for (int u = 0; u < VB; ++u) pv[u] = T(0);
+      if (i >= 0 && j >= 0 && i < N && j < N) gload<T, VB>(pcg + sbase + ((size_t)i * N + j) * VB, pv);
+#pragma unroll
+      for (int u = 0; u < VB; ++u) p_s[u][rr][cc] = pv[u];
+    }
+    __syncthreads();
+  }
+  // x of node u of the chunk at (i, j) after the round's last CG step
+  auto xat = [&](int u, const double* xq, int i, int j) -> double {
+    const int o = i * N + j;
+    if constexpr (FUSE) return fma(al_s[u], (double)p_s[u][i - i0 + 1][j - j0 + 1], xq[o]);
+    return xq[o];
+  };
+  auto gradx = [&](int u, const double* xq, int i, int j, double& gx, double& gy) {
+    const double c = xat(u, xq, i, j);
+    gx = (i < N - 1) ? xat(u, xq, i + 1, j) - c : 0.0;
+    gy = (j < N - 1) ? xat(u, xq, i, j + 1) - c : 0.0;
+  };
   const size_t vo = (size_t)(live ? v : 0) * npix;
   const double* xv = x + vo;
-  const double* dv = din + 2 * vo;
   const double* ev = ein + 2 * vo;
   if constexpr (!LAST) {
     // Phase 1: shrink once per point of the tile plus one halo row (i0-1) and column (j0-1),
@@ -1706,7 +1758,7 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
       const double* eq = ein + 2 * vqo;
       const int o = i * N + j;
       double gx, gy, ndx, ndy;
-      grad_at(xq, N, i, j, gx, gy);
+      gradx(u, xq, i, j, gx, gy);
       const double ux = gx + eq[o], uy = gy + eq[npix + o];
       shrink2(ux, uy, tau, kind, ndx, ndy);
       const double nex = ux - ndx, ney = uy - ndy;
@@ -1731,7 +1783,12 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
         if (j <= N - 2) kt -= qy_s[rw + 1][mp.u][mp.jj + 1];
         if (i >= 1) kt += qx_s[rw][mp.u][mp.jj + 1];
         if (j >= 1) kt += qy_s[rw + 1][mp.u][mp.jj];
-        const double rn = r[vo + o] + mu * kt;
+        double rv = r[vo + o];
+        if constexpr (FUSE) {
+          rv = fma(-al_s[mp.u], (double)Hp[sbase + (size_t)o * VB + mp.u], rv);
+          xout[vo + o] = xat(mp.u, xv, i, j);
+        }
+        const double rn = fma(mu, kt, rv);
         r[vo + o] = rn;
         sv = (T)rn;
       }
@@ -1748,7 +1805,7 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
     T sv = T(0);
     if (live) {
       double gx, gy, ux, uy, ndx, ndy;
-      grad_at(xv, N, i, j, gx, gy);
+      gradx(mp.u, xv, i, j, gx, gy);
       ux = gx + ev[o];
       uy = gy + ev[npix + o];
       shrink2(ux, uy, tau, kind, ndx, ndy);
@@ -1757,33 +1814,10 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
       dout[2 * vo + npix + o] = ndy;
       eout[2 * vo + o] = nex;
       eout[2 * vo + npix + o] = ney;
-      if (!LAST) {
-        // K^T(dw) at (i,j): dw_x(i-1,j) - dw_x(i,j) + dw_y(i,j-1) - dw_y(i,j)
-        double kt = 0.0;
-        if (i <= N - 2) kt -= (ndx - nex) - (dv[o] - ev[o]);
-        if (j <= N - 2) kt -= (ndy - ney) - (dv[npix + o] - ev[npix + o]);
-        if (i >= 1) {
-          const int oo = o - N;
-          double ax, ay, bx, by;
-          grad_at(xv, N, i - 1, j, ax, ay);
-          const double vx = ax + ev[oo], vy = ay + ev[npix + oo];
-          shrink2(vx, vy, tau, kind, bx, by);
-          kt += (bx - (vx - bx)) - (dv[oo] - ev[oo]);
-        }
-        if (j >= 1) {
-          const int oo = o - 1;
-          double ax, ay, bx, by;
-          grad_at(xv, N, i, j - 1, ax, ay);
-          const double vx = ax + ev[oo], vy = ay + ev[npix + oo];
-          shrink2(vx, vy, tau, kind, bx, by);
-          kt += (by - (vy - by)) - (dv[npix + oo] - ev[npix + oo]);
-        }
-        const double rn = r[vo + o] + mu * kt;
-        r[vo + o] = rn;
-        sv = (T)rn;
-      } else {
-        sv = (T)xv[o];
-      }
+      // (LAST only: the other rounds returned above) the diagnostics' sample copy of x
+      const double xn = xat(mp.u, xv, i, j);
+      if constexpr (FUSE) xout[vo + o] = xn;
+      sv = (T)xn;
     }
     p[sbase + (size_t)o * VB + mp.u] = sv;
     tl.t[rw][mp.jj][mp.u] = sv;
