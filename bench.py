@@ -331,7 +331,9 @@ def main():
     compulsory = V * n * sbytes + V * m * sbytes  # each node image read once, its sinogram written once
     as_designed = 2 * V * n * sbytes + 8 * V * m * sbytes  # image + transposed copy, 8 segment partials
     lds_bytes = sbytes * a_node * n_img * 2 * n_img * V  # m rays x N rows x 2 taps x V samples
-    tr = pmc_traffic() if not args.config and world == 1 else None
+    # per-launch PMC bytes of the forward kernel: every rank runs the same 8-node launch, so the
+    # 1-GPU passes apply at any rank count (the per-step figure below is 1-GPU only: halo traffic)
+    tr = pmc_traffic() if not args.config else None
     fwd_traffic = tr["kernels"].get(FWD_KERNEL, {}).get("hbm_bytes_per_launch") if tr else None
     if args.config:
         workload = (f"{args.config}: {n_img}^2, {V_total} graph nodes ({CONFIGS[args.config]['graph']}), "

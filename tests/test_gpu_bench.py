@@ -1,0 +1,44 @@
+"""GPU: bench.py keeps the driver contract -- one JSON line on stdout with the metric,
+the whole-job value, timing fields, roofline and (optionally) the CPU baseline and the
+strong-scaling line (task contract)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*args):
+    out = subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, capture_output=True, text=True,
+                         timeout=300, check=True).stdout
+    lines = [l for l in out.splitlines() if l.strip().startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_bench_line_contract(cuda):
+    b = _run("--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--strong", "none")
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in b, k
+    assert b["n_gpus"] == 1 and b["steps"] == 3 and b["warmup"] == 1
+    assert b["unit"] == "node-updates/s" and b["higher_is_better"] is True and b["scaling"] == "weak"
+    # value = node-updates of the whole job / timed wall time
+    assert abs(b["value"] - b["config"]["nodes"] * 1e3 / b["ms_per_step"]) <= 1e-6 * b["value"]
+    r = b["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in r, k
+    assert r["bound"] in ("hbm", "mfma") and 0 < r["frac"] <= 1
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
+    assert 0 < r["lds"]["frac"] <= 1
+    assert "workload" in b["config"] and "model" not in b["config"]
+
+
+def test_bench_config_line(cuda):
+    b = _run("--config", "C2", "--steps", "2", "--warmup", "1")
+    assert b["scaling"] == "strong" and b["config"]["nodes"] == 8 and b["config"]["image"] == 256
+    assert b["value"] > 0
