@@ -104,6 +104,7 @@ struct admm_ctx {
   Buf xs, xsT, p, pT, Hp, sino, bI, fpart, r, c, d2, e2;
   Buf dsumS;  // D = sum_j q_ij as interleaved samples (BACK_H epilogue)
   Buf x2, p2; // ping-pong partners of x (local rows) and p for the fused TV update (ADMM_TV_FUSE)
+  Buf pring;  // CG direction slots 1 .. K-1 (ADMM_TV_FUSE 2; slot 0 = p, slot K = p2)
   Buf ats;    // A^T (A xs - b) of the last update's final x (ADMM_BATCH_KEEP_X)
   bool ats_valid = false;  // ats matches x_ext's local rows
   hipGraph_t g_update_reuse = nullptr;
@@ -395,20 +396,32 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 
   double* ecur = B.e;
   double* dnxt = (double*)C->d2.p;
   double* enxt = (double*)C->e2.p;
-  // ADMM_TV_FUSE: the round's last CG step runs inside the TV update, which reads x and p
-  // over its tiles' halos while writing them: x and p ping-pong (xcur -> xnxt, p -> pnxt)
+  // ADMM_TV_FUSE 1: the round's last CG step runs inside the TV update; 2: every x step of
+  // the round does (the CG updates leave x alone and write each new direction to its own
+  // slot of a ring, p_0 .. p_K).  The TV update reads x and the directions over its tiles'
+  // halos while writing them, so x ping-pongs (xcur -> xnxt) and the restart p = r goes to
+  // the ring's spare slot.
+  const int K = B.cg_iters, Tt = rounds > 0 ? rounds : B.tv_iters;
+  const int F = !ADMM_CG_SKIP_P ? 0 : (ADMM_TV_FUSE == 2 && K <= kMaxCgRing) ? 2 : (ADMM_TV_FUSE ? 1 : 0);
   double* xcur = B.x_ext;
   double* xnxt = (double*)C->x2.p;
-  T* pnxt = (T*)C->p2.p;
-  const int K = B.cg_iters, Tt = rounds > 0 ? rounds : B.tv_iters;
+  std::vector<T*> slot(K + 1, p);
+  if (F == 1) slot[1] = (T*)C->p2.p;
+  if (F == 2) {
+    slot[K] = (T*)C->p2.p;
+    for (int k = 1; k < K; ++k) slot[k] = (T*)C->pring.p + (size_t)(k - 1) * nch * npix * VB;
+  }
+  const size_t rstride = (F == 2) ? (size_t)5 * V : 0;  // redH ring stride (one reduction per step)
   for (int t = 0; t < Tt; ++t) {
     for (int kk = 0; kk < K; ++kk) {
-      RET((launch_fwd_batch<T, VB, 0>(C, p, pT, sino, nullptr, nullptr, V, s)));
+      T* pk = (F == 2) ? slot[kk] : slot[0];
+      double* rk = redH + kk * rstride;
+      RET((launch_fwd_batch<T, VB, 0>(C, pk, pT, sino, nullptr, nullptr, V, s)));
       BackArgs<T> a{};
       a.sino = sino;
       a.out_t = Hp;
       a.part = (double*)C->partH.p;
-      a.pin = p;
+      a.pin = pk;
       a.r = r;
       a.dsum = B.dsum;
       a.dsum_s = (const T*)C->dsumS.p;
@@ -416,31 +429,48 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 
       a.lam = B.lam;
       a.mu = B.mu;
       RET((launch_back<T, VB, BACK_H>(C, a, V, s)));
-      RET(launch_reduce((double*)C->partH.p, 5 * V, Pb, redH, 1, 1, 0, s));
-      if (kk + 1 < K || !ADMM_CG_SKIP_P) {
-        hipLaunchKernelGGL((k_cg_update<T, VB, true>), cgg, dim3(kBlock), 0, s, xcur, r, p, pT, Hp, redH, N, V);
+      RET(launch_reduce((double*)C->partH.p, 5 * V, Pb, rk, 1, 1, 0, s));
+      if (kk + 1 < K) {
+        if (F == 2)
+          hipLaunchKernelGGL((k_cg_update<T, VB, true, false>), cgg, dim3(kBlock), 0, s, xcur, r, (const T*)pk, pT,
+                             Hp, rk, N, V, slot[kk + 1]);
+        else
+          hipLaunchKernelGGL((k_cg_update<T, VB, true, true>), cgg, dim3(kBlock), 0, s, xcur, r, (const T*)pk, pT,
+                             Hp, rk, N, V, pk);
         CHECK_LAUNCH();
-      } else if (!ADMM_TV_FUSE) {  // p is overwritten next (TV update / next x-update start)
-        hipLaunchKernelGGL((k_cg_update<T, VB, false>), cgg, dim3(kBlock), 0, s, xcur, r, p, pT, Hp, redH, N, V);
+      } else if (F == 0) {  // p is overwritten next (TV update / next x-update start)
+        hipLaunchKernelGGL((k_cg_update<T, VB, false, true>), cgg, dim3(kBlock), 0, s, xcur, r, (const T*)pk, pT,
+                           Hp, rk, N, V, pk);
         CHECK_LAUNCH();
       }
     }
     const bool last = (t + 1 == Tt);
-    constexpr bool F = ADMM_TV_FUSE && ADMM_CG_SKIP_P;
-    if (!last) {
-      hipLaunchKernelGGL((k_tv_update<T, VB, false, F>), tg, dim3(kBlock), 0, s, xcur, dcur, ecur, dnxt, enxt, r,
-                         F ? pnxt : p, pT, tau, B.mu, B.tv_kind, N, V, xnxt, p, Hp, redH);
-      CHECK_LAUNCH();
+    PRing<T> pr{};
+    pr.K = (F == 2) ? K : 1;
+    for (int k = 0; k < pr.K; ++k) pr.p[k] = slot[k];
+    T* pout = last ? xs : (F == 2 ? slot[K] : (F == 1 ? slot[1] : slot[0]));
+    T* poutT = last ? xsT : pT;
+    if (F) {
+      if (!last)
+        hipLaunchKernelGGL((k_tv_update<T, VB, false, true>), tg, dim3(kBlock), 0, s, xcur, dcur, ecur, dnxt, enxt,
+                           r, pout, poutT, tau, B.mu, B.tv_kind, N, V, xnxt, pr, Hp, redH);
+      else
+        hipLaunchKernelGGL((k_tv_update<T, VB, true, true>), tg, dim3(kBlock), 0, s, xcur, dcur, ecur, dnxt, enxt,
+                           r, pout, poutT, tau, B.mu, B.tv_kind, N, V, xnxt, pr, Hp, redH);
     } else {
-      hipLaunchKernelGGL((k_tv_update<T, VB, true, F>), tg, dim3(kBlock), 0, s, xcur, dcur, ecur, dnxt, enxt, r,
-                         xs, xsT, tau, B.mu, B.tv_kind, N, V, xnxt, p, Hp, redH);
-      CHECK_LAUNCH();
+      if (!last)
+        hipLaunchKernelGGL((k_tv_update<T, VB, false, false>), tg, dim3(kBlock), 0, s, xcur, dcur, ecur, dnxt,
+                           enxt, r, pout, poutT, tau, B.mu, B.tv_kind, N, V, xnxt, pr, Hp, redH);
+      else
+        hipLaunchKernelGGL((k_tv_update<T, VB, true, false>), tg, dim3(kBlock), 0, s, xcur, dcur, ecur, dnxt, enxt,
+                           r, pout, poutT, tau, B.mu, B.tv_kind, N, V, xnxt, pr, Hp, redH);
     }
+    CHECK_LAUNCH();
     std::swap(dcur, dnxt);
     std::swap(ecur, enxt);
     if (F) {
       std::swap(xcur, xnxt);
-      if (!last) std::swap(p, pnxt);
+      if (!last) std::swap(slot[0], slot[F == 2 ? K : 1]);
     }
   }
   if (xcur != B.x_ext)  // odd number of fused rounds: x ended in scratch
@@ -854,7 +884,7 @@ int admm_ctx_destroy(admm_ctx* C) {
   free_graphs(C);
   Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->op_sino, &C->op_fpart, &C->op_order[0], &C->op_order[1], &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->bI, &C->fpart, &C->r, &C->c,
                  &C->d2, &C->e2, &C->partH, &C->partS, &C->partD, &C->partE, &C->redH, &C->fg_order, &C->dsumS, &C->ats,
-                 &C->f_ptr, &C->f_idx, &C->f_val, &C->t_ptr, &C->t_idx, &C->t_val, &C->x2, &C->p2};
+                 &C->f_ptr, &C->f_idx, &C->f_val, &C->t_ptr, &C->t_idx, &C->t_val, &C->x2, &C->p2, &C->pring};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (C->fang) (void)hipFree(C->fang);
@@ -966,6 +996,8 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
     RET(ensure(C->x2, (size_t)V * npix * 8));
     RET(ensure(C->p2, Vp * npix * ds));
   }
+  if (ADMM_TV_FUSE == 2 && B.cg_iters > 1 && B.cg_iters <= kMaxCgRing)
+    RET(ensure(C->pring, (size_t)(B.cg_iters - 1) * Vp * npix * ds));
   if (B.flags & ADMM_BATCH_KEEP_X) RET(ensure(C->ats, Vp * npix * ds));
   C->ats_valid = false;
   RET(ensure(C->sino, Vp * m * ds));
@@ -987,7 +1019,7 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   RET(ensure(C->partS, (size_t)V * C->P_fwd * 8));
   RET(ensure(C->partD, (size_t)5 * V * C->P_back * 8));
   RET(ensure(C->partE, (size_t)3 * std::max(1, B.n_edges) * C->P_edge * 8));
-  RET(ensure(C->redH, (size_t)5 * V * 8));
+  RET(ensure(C->redH, (size_t)5 * V * 8 * std::max(1, std::min(B.cg_iters, kMaxCgRing))));
   C->bound = true;
   if (C->use_graph) {
     auto fu = [&](hipStream_t s) {

@@ -1578,18 +1578,21 @@ __global__ __launch_bounds__(kBlock) void k_transpose(const T* __restrict__ in, 
 constexpr int kCgRows = kBlock / kTile;  // 8 rows x 32 columns per block
 
 #ifndef ADMM_TV_FUSE
-#define ADMM_TV_FUSE 1  // the round's last CG step fused into the TV update (0: separate kernels)
+#define ADMM_TV_FUSE 1  // CG x steps applied by the TV update: 1 the round's last one, 2 all K (direction ring), 0 none
 #endif
 #ifndef ADMM_CG_SKIP_P
 #define ADMM_CG_SKIP_P 1  // 0: every CG step writes p (A/B timing only)
 #endif
 // WRITE_P = false: the last CG step of a split-Bregman round -- the TV update (or the next
 // x-update's start) overwrites p and its transposed copy, so only x and r are written
-template <typename T, int VB, bool WRITE_P = true>
+// WRITE_X = false (ADMM_TV_FUSE 2): x is left alone -- the TV update applies the round's
+// x += alpha_k p_k, k = 0..K-1, in the same order (so bitwise the same x) from the p ring;
+// p_{k+1} then goes to its own slot pout (p_k stays readable for that).
+template <typename T, int VB, bool WRITE_P = true, bool WRITE_X = true>
 __global__ __launch_bounds__(kBlock) void k_cg_update(double* __restrict__ x, double* __restrict__ r,
-                                                      T* __restrict__ p, T* __restrict__ pT,
+                                                      const T* p, T* __restrict__ pT,
                                                       const T* __restrict__ Hp, const double* __restrict__ redH,
-                                                      int N, int V) {
+                                                      int N, int V, T* pout) {
   __shared__ T tl[kCgRows][kTile + 1][VB];
   __shared__ double ab_s[VB][2];
   const int chunk = blockIdx.z, v0 = chunk * VB;
@@ -1625,14 +1628,14 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(double* __restrict__ x, do
         const size_t o = (size_t)(v0 + u) * npix + pix;
         const double alpha = ab_s[u][0], beta = ab_s[u][1];
         const double pd = (double)pv[u];
-        x[o] = fma(alpha, pd, x[o]);  // (explicit fma: k_tv_update<FUSE> repeats it bitwise)
+        if constexpr (WRITE_X) x[o] = fma(alpha, pd, x[o]);  // (explicit fma: k_tv_update<FUSE> repeats it bitwise)
         const double rn = fma(-alpha, (double)hv[u], r[o]);
         r[o] = rn;
         np[u] = (T)(rn + beta * pd);
       }
       if constexpr (WRITE_P) tl[ii][jj][u] = np[u];
     }
-    if constexpr (WRITE_P) gstore<T, VB>(p + sbase + (size_t)pix * VB, np);
+    if constexpr (WRITE_P) gstore<T, VB>(pout + sbase + (size_t)pix * VB, np);
   }
   if constexpr (!WRITE_P) return;
   __syncthreads();
@@ -1671,19 +1674,28 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
-// FUSE: the round's last CG step (k_cg_update<..., false>: x += alpha p, r -= alpha Hp) is
-// folded in.  x after that step is formed wherever the stencil reads it (tile + halo) from
-// the old x and p (pcg) with the same fma, written once to xout (x ping-pongs: neighbour
-// blocks still read the old x), and r gets both updates in one pass; the CG restart p = r
-// goes to a buffer other than pcg for the same reason.  Bitwise the same as the two
-// kernels; saves the CG update's x / r round trip through HBM and one launch per round.
+// FUSE: the round's CG x steps are folded in (ADMM_TV_FUSE 2: all K of them, the CG updates
+// leaving x alone and keeping each direction p_k in a ring slot; 1: only the last one).
+// x after those steps is formed once per pixel of the stencil region, from the old x and
+// p_k with the same fmas in the same order, written once to xout (x ping-pongs: neighbour
+// blocks still read the old x), and r gets the last step's update and the TV shift in one
+// pass; the CG restart p = r goes to a slot no one reads here.  Bitwise the same iteration
+// as the separate kernels (scripts/check_bitwise.py).
+// The CG directions whose x steps the fused TV update applies (FUSE): p[k] with alpha_k
+// from the reduction redH + k * 5V, k = 0 .. K-1 (K = 1: only the round's last step).
+constexpr int kMaxCgRing = 8;
+template <typename T>
+struct PRing {
+  const T* p[kMaxCgRing];
+  int K;
+};
 template <typename T, int VB, bool LAST, bool FUSE = false>
 __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__ x, const double* __restrict__ din,
                                                       const double* __restrict__ ein, double* __restrict__ dout,
                                                       double* __restrict__ eout, double* __restrict__ r,
                                                       T* __restrict__ p, T* __restrict__ pT, double tau,
                                                       double mu, int kind, int N, int V, double* __restrict__ xout,
-                                                      const T* __restrict__ pcg, const T* __restrict__ Hp,
+                                                      PRing<T> pr, const T* __restrict__ Hp,
                                                       const double* __restrict__ redH) {
   __shared__ TileT<T, VB> tl;
   const EwMap<VB> mp;
@@ -1693,42 +1705,50 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
   const size_t sbase = (size_t)chunk * npix * VB;
   const int wg = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
   const int i0 = (wg / gridDim.x) * EwMap<VB>::TI, j0 = (wg % gridDim.x) * kTile;
-  __shared__ double al_s[VB];
-  if constexpr (FUSE) {  // alpha of the round's last CG step (as k_cg_update)
-    if ((int)threadIdx.x < VB) {
-      const int vv = chunk * VB + threadIdx.x;
+  // FUSE: x after the round's CG steps over the block's stencil region (rows i0-1 .. i0+TI,
+  // columns j0-1 .. j0+kTile), formed once per pixel into LDS from the old x and the p ring
+  // (32-B vector loads of each p), x = fma(alpha_k, p_k, x) for k = 0 .. K-1 as the CG
+  // updates did it; the stencil then reads LDS only
+  constexpr int PR = EwMap<VB>::TI + 2, PC = kTile + 2;
+  __shared__ double al_s[FUSE ? kMaxCgRing : 1][VB];
+  __shared__ double x_s[FUSE ? VB : 1][FUSE ? PR : 1][FUSE ? PC + 1 : 1];
+  if constexpr (FUSE) {
+    if ((int)threadIdx.x < VB * pr.K) {  // alpha_k per node (as k_cg_update)
+      const int k = threadIdx.x / VB, u = threadIdx.x % VB, vv = chunk * VB + u;
       double alpha = 0.0;
       if (vv < V) {
-        const double pHp = redH[5 * vv], rp = redH[5 * vv + 4];
-        alpha = (pHp != 0.0) ? rp / pHp : 0.0;
+        const double* S = redH + (size_t)k * 5 * V + 5 * vv;
+        alpha = (S[0] != 0.0) ? S[4] / S[0] : 0.0;
       }
-      al_s[threadIdx.x] = alpha;
+      al_s[k][u] = alpha;
     }
     __syncthreads();
-  }
-  // FUSE: p over the block's stencil region (rows i0-1 .. i0+TI, columns j0-1 .. j0+kTile),
-  // staged node-major in LDS with one 32-B vector load per pixel (read per node straight from
-  // the interleaved samples, the stencil's loads were 4 B every 32 B: 65 vs 55 us)
-  constexpr int PR = EwMap<VB>::TI + 2, PC = kTile + 2;
-  __shared__ T p_s[FUSE ? VB : 1][FUSE ? PR : 1][FUSE ? PC + 1 : 1];
-  if constexpr (FUSE) {
     for (int q = threadIdx.x; q < PR * PC; q += kBlock) {
       const int rr = q / PC, cc = q % PC;
       const int i = i0 - 1 + rr, j = j0 - 1 + cc;
-      T pv[VB];
+      if (i < 0 || j < 0 || i >= N || j >= N) continue;
+      const int o = i * N + j;
+      double xn[VB];
 #pragma unroll
-      for (int u = 0; u < VB; ++u) pv[u] = T(0);
-      if (i >= 0 && j >= 0 && i < N && j < N) gload<T, VB>(pcg + sbase + ((size_t)i * N + j) * VB, pv);
+      for (int u = 0; u < VB; ++u) {
+        const int vq = chunk * VB + u;
+        xn[u] = vq < V ? x[(size_t)vq * npix + o] : 0.0;
+      }
+      for (int k = 0; k < pr.K; ++k) {
+        T pv[VB];
+        gload<T, VB>(pr.p[k] + sbase + (size_t)o * VB, pv);
 #pragma unroll
-      for (int u = 0; u < VB; ++u) p_s[u][rr][cc] = pv[u];
+        for (int u = 0; u < VB; ++u) xn[u] = fma(al_s[k][u], (double)pv[u], xn[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < VB; ++u) x_s[u][rr][cc] = xn[u];
     }
     __syncthreads();
   }
-  // x of node u of the chunk at (i, j) after the round's last CG step
+  // x of node u of the chunk at (i, j) after the round's CG steps
   auto xat = [&](int u, const double* xq, int i, int j) -> double {
-    const int o = i * N + j;
-    if constexpr (FUSE) return fma(al_s[u], (double)p_s[u][i - i0 + 1][j - j0 + 1], xq[o]);
-    return xq[o];
+    if constexpr (FUSE) return x_s[u][i - i0 + 1][j - j0 + 1];
+    return xq[i * N + j];
   };
   auto gradx = [&](int u, const double* xq, int i, int j, double& gx, double& gy) {
     const double c = xat(u, xq, i, j);
@@ -1785,7 +1805,7 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
         if (j >= 1) kt += qy_s[rw + 1][mp.u][mp.jj];
         double rv = r[vo + o];
         if constexpr (FUSE) {
-          rv = fma(-al_s[mp.u], (double)Hp[sbase + (size_t)o * VB + mp.u], rv);
+          rv = fma(-al_s[pr.K - 1][mp.u], (double)Hp[sbase + (size_t)o * VB + mp.u], rv);
           xout[vo + o] = xat(mp.u, xv, i, j);
         }
         const double rn = fma(mu, kt, rv);
