@@ -1578,7 +1578,7 @@ __global__ __launch_bounds__(kBlock) void k_transpose(const T* __restrict__ in, 
 constexpr int kCgRows = kBlock / kTile;  // 8 rows x 32 columns per block
 
 #ifndef ADMM_TV_FUSE
-#define ADMM_TV_FUSE 1  // CG x steps applied by the TV update: 1 the round's last one, 2 all K (direction ring), 0 none
+#define ADMM_TV_FUSE 2  // CG x steps applied by the TV update: 2 all K (direction ring), 1 the round's last one, 0 none
 #endif
 #ifndef ADMM_CG_SKIP_P
 #define ADMM_CG_SKIP_P 1  // 0: every CG step writes p (A/B timing only)
@@ -1734,11 +1734,15 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
         const int vq = chunk * VB + u;
         xn[u] = vq < V ? x[(size_t)vq * npix + o] : 0.0;
       }
+      // direction k + 1 is loaded before step k's fmas (one load in flight; two: 60.4 us)
+      T pa[VB], pb[VB];
+      gload<T, VB>(pr.p[0] + sbase + (size_t)o * VB, pa);
       for (int k = 0; k < pr.K; ++k) {
-        T pv[VB];
-        gload<T, VB>(pr.p[k] + sbase + (size_t)o * VB, pv);
+        if (k + 1 < pr.K) gload<T, VB>(pr.p[k + 1] + sbase + (size_t)o * VB, pb);
 #pragma unroll
-        for (int u = 0; u < VB; ++u) xn[u] = fma(al_s[k][u], (double)pv[u], xn[u]);
+        for (int u = 0; u < VB; ++u) xn[u] = fma(al_s[k][u], (double)pa[u], xn[u]);
+#pragma unroll
+        for (int u = 0; u < VB; ++u) pa[u] = pb[u];
       }
 #pragma unroll
       for (int u = 0; u < VB; ++u) x_s[u][rr][cc] = xn[u];
