@@ -317,6 +317,10 @@ def main():
 
     el = timed_steps(r, args.steps, args.warmup, world, prime)
     nb, plan, geom = r["nb"], r["plan"], r["geom"]
+    # N > 1: the halo rows the last exchange delivered (RCCL p2p / all-gather) must equal the
+    # owners' images byte for byte (checked after the timed region)
+    from admm_hip.exchange import verify_halo
+    xcheck = verify_halo(plan, nb.x_ext) if world > 1 else None
     n_img, V_total, dtype = r["n_img"], r["V_total"], r["dtype"]
     value = V_total * args.steps / el
     ms_per_step = 1e3 * el / args.steps
@@ -402,6 +406,9 @@ def main():
         },
         "roofline": roof,
     }
+    if xcheck is not None:
+        result["exchange_check"] = dict(xcheck, backend=backend, mode=r["halo"].mode,
+                                        ok=xcheck["mismatched_rows"] == 0)
     if tr and tr.get("per_step") and not args.config and world == 1:
         sb = float(tr["per_step"]["hbm_bytes"])
         gbs = sb / (ms_per_step * 1e-3) / 1e9

@@ -138,3 +138,37 @@ def gather_images(plan: ShardPlan, x_local: torch.Tensor, group=None) -> torch.T
     lo = plan.local_nodes[0] if plan.local_nodes else 0
     buf[lo:lo + plan.V].copy_(x_local)
     return _all_reduce_sum(buf, group)
+
+
+def _row_digest(rows: torch.Tensor) -> torch.Tensor:
+    """Per-row int64 digest of the rows' bytes (position-weighted, wrapping int64 sums):
+    equal bytes give equal digests, any changed element changes it almost surely."""
+    v = rows.contiguous().view(torch.int64) if rows.dtype == torch.float64 else \
+        rows.contiguous().view(torch.int32).to(torch.int64)
+    w = torch.arange(v.shape[1], device=v.device, dtype=torch.int64) * 2 + 1
+    return (v * w).sum(dim=1)
+
+
+def verify_halo(plan: ShardPlan, x_ext: torch.Tensor, group=None) -> dict:
+    """Check that every halo row of ``x_ext`` holds, byte for byte, the owner rank's
+    current image of that node (what ``HaloExchange.run`` must deliver, by p2p or
+    all-gather).  Each rank contributes the digests of its own nodes to one table
+    (one all-reduce; exactly one rank writes each entry) and compares its halo rows.
+    Returns {"halo_rows", "mismatched_rows"} summed over ranks."""
+    if plan.world == 1:
+        return {"halo_rows": 0, "mismatched_rows": 0}
+    dev = x_ext.device
+    tbl = torch.zeros(plan.V_total, dtype=torch.int64, device=dev)
+    lo = plan.local_nodes[0] if plan.local_nodes else 0
+    if plan.V:
+        tbl[lo:lo + plan.V] = _row_digest(x_ext[: plan.V])
+    _all_reduce_sum(tbl, group)
+    bad = 0
+    if plan.halo_nodes:
+        rows = torch.tensor([plan.xrow[g] for g in plan.halo_nodes], dtype=torch.long, device=dev)
+        want = tbl[torch.tensor(plan.halo_nodes, dtype=torch.long, device=dev)]
+        bad = int((_row_digest(x_ext.index_select(0, rows)) != want).sum().item())
+    counts = torch.tensor([len(plan.halo_nodes), bad], dtype=torch.int64, device=dev)
+    _all_reduce_sum(counts, group)
+    return {"halo_rows": int(counts[0].item()), "mismatched_rows": int(counts[1].item())}
+

@@ -242,3 +242,54 @@ def test_operators_follow_each_ranks_current_device():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res == {0: [0] * 6, 1: [1] * 6}
+
+
+def _halo_check_rank(rank, world, port, gname, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "distributed-inverse-problem-admm_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from admm_hip.exchange import HaloExchange, verify_halo
+        G = dict(graphs())[gname]
+        V = G.number_of_nodes()
+        plan = make_plan(G, V, world, rank)
+        n = 37
+        x = torch.zeros((plan.n_xext, n), dtype=torch.float64)
+        for g in plan.local_nodes:  # node g's image: a function of g only
+            x[plan.xrow[g]] = torch.from_numpy(np.random.default_rng(g).standard_normal(n))
+        before = verify_halo(plan, x)  # halo rows still zero
+        HaloExchange(plan, x).run()
+        after = verify_halo(plan, x)
+        if plan.halo_nodes:  # one flipped bit in one halo row
+            x[plan.xrow[plan.halo_nodes[0]]].view(torch.int64)[3] ^= 1
+        flipped = verify_halo(plan, x)
+        q.put((rank, (before, after, flipped, len(plan.halo_nodes))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("gname,world", [("ring8", 2), ("complete6", 2), ("ring8", 4)])
+def test_verify_halo_detects_exchange_errors(gname, world):
+    """bench.py's N > 1 exchange check (admm_hip.exchange.verify_halo): after HaloExchange.run
+    every halo row equals its owner's row byte for byte; before it, or with one bit
+    flipped, the check reports the rows."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_halo_check_rank, args=(r, world, port, gname, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    total = sum(res[r][3] for r in range(world))
+    flips = sum(1 for r in range(world) if res[r][3])
+    for r in range(world):
+        before, after, flipped, _ = res[r]
+        assert before == {"halo_rows": total, "mismatched_rows": total}
+        assert after == {"halo_rows": total, "mismatched_rows": 0}
+        assert flipped == {"halo_rows": total, "mismatched_rows": flips}
