@@ -1,5 +1,5 @@
 # Full GPU check of the in-tree library: every -m gpu test, then HBM traffic passes,
-# kernel-trace stats and the default bench line (with the CPU baseline).  usage: g5.sh TAG
+# kernel-trace stats and the default bench line (with the CPU baseline).  usage: gpu_full_check.sh TAG
 set -u
 mkdir -p gpurun_out
 TAG=${1:-r2}
