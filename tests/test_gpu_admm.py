@@ -124,6 +124,18 @@ def test_odd_tv_rounds_and_single_cg(cuda):
     compare(nx.path_graph(3), 24, 3, 4, 72, tv_iters=3, cg_iters=1)
 
 
+def test_ragged_image_and_node_chunks(cuda):
+    """N = 37 (partial 32-pixel tiles everywhere) and V = 11 (one full 8-node chunk and a
+    ragged 3-node one) through the whole loop."""
+    compare(nx.cycle_graph(11), 37, 11, 4, 11 * 20)
+
+
+def test_cg_steps_beyond_the_direction_ring(cuda):
+    """cg_iters = 9 > the 8-slot direction ring: the TV update then folds in only the round's
+    last CG step (ADMM_TV_FUSE 1 path) -- same iteration, same oracle."""
+    compare(nx.cycle_graph(4), 32, 4, 3, 96, tv_iters=2, cg_iters=9)
+
+
 def test_deterministic_bitwise(cuda):
     ops, ph, sinos, Wi, Q, A, _ = setup_problem(48, 4, 96)
     G = nx.cycle_graph(4)
