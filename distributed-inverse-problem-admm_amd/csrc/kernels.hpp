@@ -501,7 +501,10 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
                                                  int N, int n_det, int n_ang, int V) {
   constexpr int NPL = Planes<T, VB>::NPL, PV = Planes<T, VB>::PV;
   constexpr int PER = (kFgRows * kFgWin * NPL + kFgThreads - 1) / kFgThreads;  // staged packs per thread
-  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  // g (the wave's angle slot) is wave-uniform: readfirstlane lets the compiler keep it, and
+  // everything derived from it (group offsets, DMA piece indices, the idle test), in SGPRs
+  // with scalar branches instead of VALU compares and EXEC masking
+  const int lane = threadIdx.x & 63, g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   // 1-D grid over a host-ordered block table (order[b] = {chunk of rays, group, seg +
   // kFgSeg * node chunk}): heavy (large-G) blocks first, paired with light ones on a CU
   const int4 ob = order[blockIdx.x];
@@ -606,7 +609,11 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   // the chunk's window origins, read once into scalar registers (a per-row LDS read
   // would put a dependent LDS round trip in front of every row's tap reads)
   auto origins = [&](int m0, int (&wl)[R]) {
-    if constexpr (ADMM_FG_W4 && R == 4) {
+    if constexpr (ADMM_FG_W4 && R == 2) {  // one LDS round trip for both rows
+      const int2 w2 = *reinterpret_cast<const int2*>(&wlo_s[m0 - m_lo]);
+      wl[0] = w2.x;
+      wl[1] = w2.y;
+    } else if constexpr (ADMM_FG_W4 && R == 4) {
       const int4 w4 = *reinterpret_cast<const int4*>(&wlo_s[m0 - m_lo]);
       wl[0] = __builtin_amdgcn_readfirstlane(w4.x);
       wl[1] = __builtin_amdgcn_readfirstlane(w4.y);
@@ -684,11 +691,23 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         w1 = (T)(l - fl);
       }
       const T w0 = T(1) - w1;
-      const bool odd = idx & 1;
       se[r] = (idx + 1) >> 1;
       so[r] = kFgOdd + (idx >> 1);
-      we[r] = odd ? w1 : w0;
-      wo[r] = odd ? w0 : w1;
+      if constexpr (std::is_same<T, float>::value) {
+        // parity mask (0 / -1) and two bitfield selects: 3 VALU instead of and + compare +
+        // 2 conditional moves (same values, bit for bit)
+        const int msk = __builtin_amdgcn_sbfe(idx, 0, 1);
+        const int i0 = __float_as_int(w0), i1 = __float_as_int(w1);
+        int ie, io;
+        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(ie) : "v"(msk), "v"(i1), "v"(i0));
+        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(io) : "v"(msk), "v"(i0), "v"(i1));
+        we[r] = __int_as_float(ie);
+        wo[r] = __int_as_float(io);
+      } else {
+        const bool odd = idx & 1;
+        we[r] = odd ? w1 : w0;
+        wo[r] = odd ? w0 : w1;
+      }
     }
     Pack<T, PV> cur[2 * NPL], nxt[2 * NPL];
 #pragma unroll
@@ -752,8 +771,12 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
     };
     if (ADMM_FG_EXPT != 2) dma(m_lo, 0);
     __syncthreads();  // (its fence waits for this wave's LDS-DMA: vmcnt(0)) chunk 0 staged
-    for (int m0 = m_lo, ci = 0; m0 < m_hi; m0 += R, ++ci) {
-      const int cb = ci & 1;
+    // one chunk: DMA of the next one into the other buffer, then this one's taps.  The
+    // buffer index is a compile-time constant (the loop is unrolled by the two buffers), so
+    // the LDS base of every tap read folds into the ds_read offset field instead of costing
+    // two VALU adds per row (the kernel is VALU-issue bound)
+    auto step = [&](auto cbc, int m0) __attribute__((always_inline)) {
+      constexpr int cb = decltype(cbc)::value;
       // the other buffer was last read by the previous chunk's taps (done: barrier below)
       if (ADMM_FG_EXPT != 2 && m0 + R < m_hi) dma(m0 + R, cb ^ 1);
       origins(m0, wl_cur);
@@ -763,6 +786,10 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       else
         taps(win[cb], m0, rows, wl_cur);
       __syncthreads();  // this chunk's readers done; next chunk's DMA landed (vmcnt(0) + barrier)
+    };
+    for (int m0 = m_lo; m0 < m_hi; m0 += 2 * R) {
+      step(std::integral_constant<int, 0>{}, m0);
+      if (m0 + R < m_hi) step(std::integral_constant<int, 1>{}, m0 + R);
     }
   } else {
     // staging in two halves: issue global loads for chunk c+1 into registers
