@@ -450,24 +450,44 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 
     for (int k = 0; k < pr.K; ++k) pr.p[k] = slot[k];
     T* pout = last ? xs : (F == 2 ? slot[K] : (F == 1 ? slot[1] : slot[0]));
     T* poutT = last ? xsT : pT;
+    // split-Bregman state in/out of this round: d, e (B.d / B.e or the scratch pair) or,
+    // between the rounds of the update (ADMM_TV_USTATE, Tt > 1), u = Kx + e in ua / ub
+    const bool uin = ADMM_TV_USTATE && t > 0 && Tt > 1;
+    const bool uout = ADMM_TV_USTATE && !last && Tt > 1;
+    double* ua = (double*)C->d2.p;
+    double* ub = (double*)C->e2.p;
+    const double* din = uin ? ((t % 2) ? ua : ub) : dcur;
+    const double* ein = ecur;  // (not read when uin)
+    double* dout = uout ? ((t % 2) ? ub : ua) : (ADMM_TV_USTATE && Tt > 1 ? B.d : dnxt);
+    double* eout = uout ? nullptr : (ADMM_TV_USTATE && Tt > 1 ? B.e : enxt);
+#define TV_LAUNCH(LASTV, FUSEV, UINV, UOUTV)                                                                     \
+  hipLaunchKernelGGL((k_tv_update<T, VB, LASTV, FUSEV, UINV, UOUTV>), tg, dim3(kBlock), 0, s, xcur, din, ein, dout, \
+                     eout, r, pout, poutT, tau, B.mu, B.tv_kind, N, V, xnxt, pr, Hp, redH)
     if (F) {
-      if (!last)
-        hipLaunchKernelGGL((k_tv_update<T, VB, false, true>), tg, dim3(kBlock), 0, s, xcur, dcur, ecur, dnxt, enxt,
-                           r, pout, poutT, tau, B.mu, B.tv_kind, N, V, xnxt, pr, Hp, redH);
-      else
-        hipLaunchKernelGGL((k_tv_update<T, VB, true, true>), tg, dim3(kBlock), 0, s, xcur, dcur, ecur, dnxt, enxt,
-                           r, pout, poutT, tau, B.mu, B.tv_kind, N, V, xnxt, pr, Hp, redH);
+      if (!last) {
+        if (uin) TV_LAUNCH(false, true, true, true);
+        else if (uout) TV_LAUNCH(false, true, false, true);
+        else TV_LAUNCH(false, true, false, false);
+      } else {
+        if (uin) TV_LAUNCH(true, true, true, false);
+        else TV_LAUNCH(true, true, false, false);
+      }
     } else {
-      if (!last)
-        hipLaunchKernelGGL((k_tv_update<T, VB, false, false>), tg, dim3(kBlock), 0, s, xcur, dcur, ecur, dnxt,
-                           enxt, r, pout, poutT, tau, B.mu, B.tv_kind, N, V, xnxt, pr, Hp, redH);
-      else
-        hipLaunchKernelGGL((k_tv_update<T, VB, true, false>), tg, dim3(kBlock), 0, s, xcur, dcur, ecur, dnxt, enxt,
-                           r, pout, poutT, tau, B.mu, B.tv_kind, N, V, xnxt, pr, Hp, redH);
+      if (!last) {
+        if (uin) TV_LAUNCH(false, false, true, true);
+        else if (uout) TV_LAUNCH(false, false, false, true);
+        else TV_LAUNCH(false, false, false, false);
+      } else {
+        if (uin) TV_LAUNCH(true, false, true, false);
+        else TV_LAUNCH(true, false, false, false);
+      }
     }
+#undef TV_LAUNCH
     CHECK_LAUNCH();
-    std::swap(dcur, dnxt);
-    std::swap(ecur, enxt);
+    if (!(ADMM_TV_USTATE && Tt > 1)) {
+      std::swap(dcur, dnxt);
+      std::swap(ecur, enxt);
+    }
     if (F) {
       std::swap(xcur, xnxt);
       if (!last) std::swap(slot[0], slot[F == 2 ? K : 1]);
@@ -475,7 +495,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 
   }
   if (xcur != B.x_ext)  // odd number of fused rounds: x ended in scratch
     HIPCHK(hipMemcpyAsync(B.x_ext, xcur, (size_t)V * npix * sizeof(double), hipMemcpyDeviceToDevice, s));
-  if (dcur != B.d) {  // odd number of rounds: state ended in scratch
+  if (dcur != B.d) {  // odd number of d / e rounds: state ended in scratch
     HIPCHK(hipMemcpyAsync(B.d, dcur, 2 * V * npix * sizeof(double), hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(B.e, ecur, 2 * V * npix * sizeof(double), hipMemcpyDeviceToDevice, s));
   }
