@@ -699,10 +699,9 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
     ba[t].L = h / std::fabs(al);
     bc[t].Bi = ba[t].Bi;
     bc[t].Bj = ba[t].Bj;
-    bc[t].sLf = (float)(ba[t].slope * ba[t].L);
-    bc[t].Lf = (float)ba[t].L;
-    bc[t].LmsLf = (float)(ba[t].L - ba[t].slope * ba[t].L);
-    bc[t].pad = 0.f;
+    const float sLf = (float)(ba[t].slope * ba[t].L);
+    bc[t].ws = float2v{-sLf, sLf};
+    bc[t].wc = float2v{(float)ba[t].L, (float)(ba[t].L - ba[t].slope * ba[t].L)};
   }
   // angle groups for the grouped forward projector: consecutive angles of one case,
   // G <= kFgG, whose union row window of every 64-ray chunk fits kFgWin (float64, same

@@ -52,10 +52,12 @@ struct BackAngle {
 
 // Compact per-angle record of the back projector's hot loop (one s_load_dwordx8):
 // k_f = (i - c0) Bi + (j - c0) Bj + K with K = -det_min/hd - 1/2 the same for every
-// angle; float32 weights w0 = max(0, L - f sL), w1 = max(0, (L - sL) + f sL).
+// angle; float32 weights w0 = max(0, L - f sL), w1 = max(0, (L - sL) + f sL), formed
+// as one packed fma (f, f) * ws + wc with ws = (-sL, sL), wc = (L, L - sL).
+typedef float float2v __attribute__((ext_vector_type(2)));
 struct alignas(32) BackAngleC {
   double Bi, Bj;
-  float sLf, Lf, LmsLf, pad;
+  float2v ws, wc;
 };
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
@@ -1245,8 +1247,10 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
     const int k0 = (int)kfl;
     const T f = (T)(kf - kfl);
     if constexpr (std::is_same<T, float>::value) {
-      w0 = fmaxf(0.f, fmaf(-f, g.sLf, g.Lf));
-      w1 = fmaxf(0.f, fmaf(f, g.sLf, g.LmsLf));
+      // one v_pk_fma_f32 for both taps (bitwise the two scalar fmas: f * (-sL) == (-f) * sL)
+      const float2v w = __builtin_elementwise_fma(float2v{f, f}, g.ws, g.wc);
+      w0 = fmaxf(0.f, w.x);
+      w1 = fmaxf(0.f, w.y);
     } else {
       const BackAngle& gd = A.ang[t0c + tt];
       w0 = fmax(T(0), T(1) - f * (T)gd.slope) * (T)gd.L;
