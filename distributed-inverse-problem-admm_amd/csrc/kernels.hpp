@@ -1233,14 +1233,17 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
   // window stays at 48 KB of LDS
   constexpr int ANGC = (NPL > 2) ? kBAngC / 2 : kBAngC;
   __shared__ Pack<T, PV> win[NPL][(MODE == BACK_WSQ) ? 1 : ANGC][kBWin];
-  __shared__ int4 kmin_s[2][ANGC / 4];
+  __shared__ int4 kmin_s[2][ANGC / 4];  // per angle: window byte offset koff (see tap)
   T acc[VB];
 #pragma unroll
   for (int u = 0; u < VB; ++u) acc[u] = T(0);
   const T* sino_c = A.sino + (size_t)chunk * m_rays * VB;
   int t0c = 0;  // first angle of the current chunk (float64 weight path)
 
-  auto tap = [&](const BackAngleC& g, int kmin, T& w0, T& w1, Pack<T, PV> (&s0)[NPL], Pack<T, PV> (&s1)[NPL],
+  // window taps address LDS by byte offset: koff = (slot * kBWin - kmin) * sizeof(Pack) is formed
+  // once per angle and chunk (kmin_chunk), so a tap's address is one v_lshl_add of k0
+  constexpr int PB = (int)sizeof(Pack<T, PV>);
+  auto tap = [&](const BackAngleC& g, int koff, T& w0, T& w1, Pack<T, PV> (&s0)[NPL], Pack<T, PV> (&s1)[NPL],
                  int tt) {
     const double kf = fma(xi, g.Bi, fma(yj, g.Bj, Kc));
     const double kfl = floor(kf);
@@ -1248,7 +1251,10 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
     const T f = (T)(kf - kfl);
     if constexpr (std::is_same<T, float>::value) {
       // one v_pk_fma_f32 for both taps (bitwise the two scalar fmas: f * (-sL) == (-f) * sL)
-      const float2v w = __builtin_elementwise_fma(float2v{f, f}, g.ws, g.wc);
+      // wc to VGPRs by one v_mov_b64 (the compiler emits two v_mov_b32; VOP3P reads one SGPR pair)
+      float2v wc;
+      asm("v_mov_b64 %0, %1" : "=v"(wc) : "s"(g.wc));
+      const float2v w = __builtin_elementwise_fma(float2v{f, f}, g.ws, wc);
       w0 = fmaxf(0.f, w.x);
       w1 = fmaxf(0.f, w.y);
     } else {
@@ -1260,11 +1266,12 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
       w0 = (k0 >= 0 && k0 <= n_det - 1) ? w0 : T(0);
       w1 = (k0 >= -1 && k0 <= n_det - 2) ? w1 : T(0);
     } else {
-      const int idx = k0 - kmin;
+      const int off = k0 * PB + koff;
 #pragma unroll
       for (int q = 0; q < NPL; ++q) {
-        s0[q] = win[q][tt][idx];
-        s1[q] = win[q][tt][idx + 1];
+        const char* wb = reinterpret_cast<const char*>(&win[q][0][0]) + off;
+        s0[q] = *reinterpret_cast<const Pack<T, PV>*>(wb);
+        s1[q] = *reinterpret_cast<const Pack<T, PV>*>(wb + PB);
       }
     }
   };
@@ -1298,7 +1305,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
       const BackAngleC g = A.angc[t0 + threadIdx.x];
       auto kf = [&](int ii, int jj) { return fma((double)ii - c0, g.Bi, fma((double)jj - c0, g.Bj, Kc)); };
       const double kmn = fmin(fmin(kf(ib, jb), kf(ib, jhi)), fmin(kf(ihi, jb), kf(ihi, jhi)));
-      reinterpret_cast<int*>(kmin_s[buf])[threadIdx.x] = (int)floor(kmn) - 1;
+      reinterpret_cast<int*>(kmin_s[buf])[threadIdx.x] = ((int)threadIdx.x * kBWin - ((int)floor(kmn) - 1)) * PB;
     }
   };
   auto wfetch = [&](int t0, int buf) {
@@ -1308,7 +1315,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
       const int q = threadIdx.x + e * kBkThreads;
       const int pl = q % NPL, aw = q / NPL;
       const int a = aw / kBWin, w = aw - a * kBWin;
-      const int k = (a < nt) ? reinterpret_cast<const int*>(kmin_s[buf])[a] + w : -1;
+      const int k = (a < nt) ? a * kBWin - reinterpret_cast<const int*>(kmin_s[buf])[a] / PB + w : -1;
       if (ADMM_BK_EXPT != 2 && a < nt && k >= 0 && k < n_det) {
         wst[e] = *reinterpret_cast<const Pack<T, PV>*>(sino_c + ((size_t)(t0 + a) * n_det + k) * VB + pl * PV);
       } else {
