@@ -74,6 +74,8 @@ struct admm_ctx {
   BackAngle* bang = nullptr;
   BackAngleC* bangc = nullptr;
   double Kb = 0.0;  // angle-independent part of the back projector's k_f
+  int kbias = 0;    // integer bias making every pixel's k_f positive (k_back)
+  int wexp = 0;     // k_back float weights scaled by 2^-wexp (<= 1 for the fma clamp)
   FgGroup* groups = nullptr;  // angle groups of the grouped forward projector (active plan)
   int n_groups = 0;           // 0: geometry does not fit the grouped kernel -> k_fwd
   int fg_nkc = 0;             // grid.x of the grouped kernel: most chunks of any (group, segment)
@@ -296,6 +298,8 @@ int launch_back(admm_ctx* C, BackArgs<T> a, int V, hipStream_t s) {
   a.ang = C->bang;
   a.angc = C->bangc;
   a.K = C->Kb;
+  a.kbias = C->kbias;
+  a.wexp = C->wexp;
   a.N = C->g.N;
   a.n_det = C->g.n_det;
   a.n_ang = C->g.n_angles;
@@ -702,6 +706,16 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
     const float sLf = (float)(ba[t].slope * ba[t].L);
     bc[t].ws = float2v{-sLf, sLf};
     bc[t].wc = float2v{(float)ba[t].L, (float)(ba[t].L - ba[t].slope * ba[t].L)};
+    while (std::ldexp((double)bc[t].wc.x, -C->wexp) > 1.0) ++C->wexp;
+    // smallest k_f of any pixel at this angle: Kb - c0 (|Bi| + |Bj|)
+    const double kmn = C->Kb - c0 * (std::fabs(ba[t].Bi) + std::fabs(ba[t].Bj));
+    C->kbias = std::max(C->kbias, (int)std::ceil(-kmn) + 2);
+  }
+  if (C->wexp != 0) {  // exact power-of-two scaling (N < 3: L = 2 / (N |cos|) can exceed 1)
+    for (int t = 0; t < g.n_angles; ++t) {
+      bc[t].ws = float2v{std::ldexp(bc[t].ws.x, -C->wexp), std::ldexp(bc[t].ws.y, -C->wexp)};
+      bc[t].wc = float2v{std::ldexp(bc[t].wc.x, -C->wexp), std::ldexp(bc[t].wc.y, -C->wexp)};
+    }
   }
   // angle groups for the grouped forward projector: consecutive angles of one case,
   // G <= kFgG, whose union row window of every 64-ray chunk fits kFgWin (float64, same

@@ -920,6 +920,8 @@ struct BackArgs {
   const BackAngle* ang;     // [n_ang]
   const BackAngleC* angc;   // [n_ang] compact records
   double K;                 // angle-independent part of k_f
+  int kbias;                // integer added to every k_f so that k_f > 0 (host: from the geometry)
+  int wexp;                 // float weights of angc are scaled by 2^-wexp so that they are <= 1
   int N, n_det, n_ang, V;
   // explicit-matrix contexts (admm_ctx_create_matrix): A^T as CSR, one row per pixel
   const int* csr_ptr;       // [n + 1]
@@ -1227,7 +1229,11 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
   const double c0 = 0.5 * (N - 1);
   const double xi = (double)min(i, N - 1) - c0, yj = (double)min(j, N - 1) - c0;
   const int jhi = min(jb + kBTJ - 1, N - 1), ihi = min(ib + kBTI - 1, N - 1);
-  const double Kc = A.K;
+  // bin positions are biased by an integer (admm_ctx: smallest k_f of any pixel, negated, + 2),
+  // so k_f > 0: floor is the truncating convert and the tap fraction one v_fract_f64; window
+  // offsets and the staged bins take the same bias
+  const int kbias = A.kbias;
+  const double Kc = A.K + (double)kbias;
 
   // angles per staged chunk: halved for 64-B sample vectors (8 float64 nodes) so the
   // window stays at 48 KB of LDS
@@ -1246,25 +1252,27 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
   auto tap = [&](const BackAngleC& g, int koff, T& w0, T& w1, Pack<T, PV> (&s0)[NPL], Pack<T, PV> (&s1)[NPL],
                  int tt) {
     const double kf = fma(xi, g.Bi, fma(yj, g.Bj, Kc));
-    const double kfl = floor(kf);
-    const int k0 = (int)kfl;
-    const T f = (T)(kf - kfl);
+    const int k0 = (int)kf;  // == floor(kf): kf > 0
+    const T f = (T)__builtin_amdgcn_fract(kf);
     if constexpr (std::is_same<T, float>::value) {
       // one v_pk_fma_f32 for both taps (bitwise the two scalar fmas: f * (-sL) == (-f) * sL)
-      // wc to VGPRs by one v_mov_b64 (the compiler emits two v_mov_b32; VOP3P reads one SGPR pair)
-      float2v wc;
+      // wc to VGPRs by one v_mov_b64 (the compiler emits two v_mov_b32; VOP3P reads one SGPR
+      // pair).  max(0, w) is the fma's clamp to [0, 1]: the host scales ws, wc by 2^-wexp so
+      // that w <= L 2^-wexp <= 1 (wexp = 0 for N >= 3), undone exactly after the angle loop
+      float2v wc, fv, w;
       asm("v_mov_b64 %0, %1" : "=v"(wc) : "s"(g.wc));
-      const float2v w = __builtin_elementwise_fma(float2v{f, f}, g.ws, wc);
-      w0 = fmaxf(0.f, w.x);
-      w1 = fmaxf(0.f, w.y);
+      fv.x = f;  // op_sel_hi:[0,...] reads the low half for both lanes of the pair
+      asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] clamp" : "=v"(w) : "v"(fv), "s"(g.ws), "v"(wc));
+      w0 = w.x;
+      w1 = w.y;
     } else {
       const BackAngle& gd = A.ang[t0c + tt];
       w0 = fmax(T(0), T(1) - f * (T)gd.slope) * (T)gd.L;
       w1 = fmax(T(0), T(1) - (T(1) - f) * (T)gd.slope) * (T)gd.L;
     }
     if constexpr (MODE == BACK_WSQ) {
-      w0 = (k0 >= 0 && k0 <= n_det - 1) ? w0 : T(0);
-      w1 = (k0 >= -1 && k0 <= n_det - 2) ? w1 : T(0);
+      w0 = (k0 >= kbias && k0 <= kbias + n_det - 1) ? w0 : T(0);
+      w1 = (k0 >= kbias - 1 && k0 <= kbias + n_det - 2) ? w1 : T(0);
     } else {
       const int off = k0 * PB + koff;
 #pragma unroll
@@ -1315,7 +1323,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
       const int q = threadIdx.x + e * kBkThreads;
       const int pl = q % NPL, aw = q / NPL;
       const int a = aw / kBWin, w = aw - a * kBWin;
-      const int k = (a < nt) ? a * kBWin - reinterpret_cast<const int*>(kmin_s[buf])[a] / PB + w : -1;
+      const int k = (a < nt) ? a * kBWin - reinterpret_cast<const int*>(kmin_s[buf])[a] / PB + w - kbias : -1;
       if (ADMM_BK_EXPT != 2 && a < nt && k >= 0 && k < n_det) {
         wst[e] = *reinterpret_cast<const Pack<T, PV>*>(sino_c + ((size_t)(t0 + a) * n_det + k) * VB + pl * PV);
       } else {
@@ -1413,6 +1421,13 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
     }
   }
 
+  if constexpr (std::is_same<T, float>::value && !CSR) {
+    if (A.wexp != 0) {  // undo the weight scaling (a power of two: exact)
+      const int e = (MODE == BACK_WSQ) ? 2 * A.wexp : A.wexp;
+#pragma unroll
+      for (int u = 0; u < VB; ++u) acc[u] = ldexpf(acc[u], e);
+    }
+  }
   double pq[VB][NQ];
 #pragma unroll
   for (int u = 0; u < VB; ++u)
