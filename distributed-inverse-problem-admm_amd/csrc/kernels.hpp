@@ -152,6 +152,36 @@ __device__ __forceinline__ void block_reduce(double (&v)[NQ], double* lds /* >= 
 // the NW waves are combined in LDS in a fixed pairwise tree.  On return thread t < NV of the
 // block can read total t from out_lds[t].  Fixed order -> bitwise reproducible.
 // ---------------------------------------------------------------------------
+#ifndef ADMM_RS_DPP
+#define ADMM_RS_DPP 1  // reduce-scatter by gfx950 permlane swaps + DPP (0: __shfl_xor / ds_bpermute)
+#endif
+// float64 lane exchange by DPP (two 32-bit moves); CTRL must describe an exact xor pairing
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, x);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)b, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+// x, y := the permlane swap of x and y (per 32-bit half): SWAP32 exchanges lanes 32-63 of x
+// with lanes 0-31 of y, otherwise odd 16-lane rows of x with even rows of y
+template <bool SWAP32>
+__device__ __forceinline__ void permswap_d(double& x, double& y) {
+  const uint64_t bx = __builtin_bit_cast(uint64_t, x), by = __builtin_bit_cast(uint64_t, y);
+  uint32_t xl = (uint32_t)bx, xh = (uint32_t)(bx >> 32), yl = (uint32_t)by, yh = (uint32_t)(by >> 32);
+  if constexpr (SWAP32) {
+    const auto l = __builtin_amdgcn_permlane32_swap(xl, yl, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(xh, yh, false, false);
+    xl = l[0]; yl = l[1]; xh = h[0]; yh = h[1];
+  } else {
+    const auto l = __builtin_amdgcn_permlane16_swap(xl, yl, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(xh, yh, false, false);
+    xl = l[0]; yl = l[1]; xh = h[0]; yh = h[1];
+  }
+  x = __builtin_bit_cast(double, ((uint64_t)xh << 32) | xl);
+  y = __builtin_bit_cast(double, ((uint64_t)yh << 32) | yl);
+}
+
 template <int NV, int NW = 4>
 __device__ __forceinline__ void block_reduce_rs(double (&v)[NV], double* lds /* >= NW*NV */,
                                                 double* out_lds /* >= NV */) {
@@ -159,6 +189,44 @@ __device__ __forceinline__ void block_reduce_rs(double (&v)[NV], double* lds /* 
   static_assert(NV % 16 == 0, "NV must be a multiple of 16");
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
+  if constexpr (ADMM_RS_DPP) {
+    // the same pairings and additions as the shuffle form below (each level an exact xor
+    // partner; a + b == b + a), so bitwise the same totals, with no LDS traffic and no selects
+    // at offsets 32 and 16: after the swap, lane i of x + y is (keep + partner's send)
+#pragma unroll
+    for (int k = 0; k < NV / 2; ++k) {
+      double x = v[k], y = v[NV / 2 + k];
+      permswap_d<true>(x, y);
+      v[k] = x + y;
+    }
+#pragma unroll
+    for (int k = 0; k < NV / 4; ++k) {
+      double x = v[k], y = v[NV / 4 + k];
+      permswap_d<false>(x, y);
+      v[k] = x + y;
+    }
+    const bool h8 = lane & 8, h4 = lane & 4;
+#pragma unroll
+    for (int k = 0; k < NV / 8; ++k) {  // xor 8 = row_ror:8 within a 16-lane row
+      const double send = h8 ? v[k] : v[NV / 8 + k];
+      const double keep = h8 ? v[NV / 8 + k] : v[k];
+      v[k] = keep + dpp_d<0x128>(send);
+    }
+#pragma unroll
+    for (int k = 0; k < NV / 16; ++k) {  // xor 4: row_shl:4 for lanes with bit 2 clear, row_shr:4 else
+      const double send = h4 ? v[k] : v[NV / 16 + k];
+      const double keep = h4 ? v[NV / 16 + k] : v[k];
+      const double up = dpp_d<0x104>(send), dn = dpp_d<0x114>(send);
+      v[k] = keep + (h4 ? dn : up);
+    }
+#pragma unroll
+    for (int k = 0; k < NV / 16; ++k) {  // xor 2, xor 1: quad_perm [2,3,0,1], [1,0,3,2]
+      double s = v[k];
+      s += dpp_d<0x4E>(s);
+      s += dpp_d<0xB1>(s);
+      v[k] = s;
+    }
+  } else {
 #pragma unroll
   for (int k = 0; k < NV / 2; ++k) {
     const bool hi = lane & 32;
@@ -193,6 +261,7 @@ __device__ __forceinline__ void block_reduce_rs(double (&v)[NV], double* lds /* 
     s += __shfl_xor(s, 2, 64);
     s += __shfl_xor(s, 1, 64);
     v[k] = s;
+  }
   }
   if ((lane & 3) == 0) {
     const int base = ((lane >> 5) & 1) * (NV / 2) + ((lane >> 4) & 1) * (NV / 4) + ((lane >> 3) & 1) * (NV / 8) +
