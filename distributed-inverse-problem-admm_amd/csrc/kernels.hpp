@@ -121,39 +121,8 @@ __device__ __forceinline__ void gstore(T* __restrict__ p, const T (&o)[VB]) {
 // deterministic block reduction of NQ float64 values per thread (256 threads);
 // result valid in thread 0.  Fixed shuffle tree + fixed LDS order.
 // ---------------------------------------------------------------------------
-template <int NQ>
-__device__ __forceinline__ void block_reduce(double (&v)[NQ], double* lds /* >= 4*NQ */) {
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    double s = v[q];
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-    v[q] = s;
-  }
-  const int wid = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) lds[wid * NQ + q] = v[q];
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) v[q] = ((lds[q] + lds[NQ + q]) + (lds[2 * NQ + q] + lds[3 * NQ + q]));
-  }
-  __syncthreads();
-}
-
-// ---------------------------------------------------------------------------
-// deterministic block reduction of NV (multiple of 16) float64 values per thread
-// by a wave-level reduce-scatter butterfly: at offsets 32, 16, 8, 4 every lane
-// keeps half of its values and adds its partner's copy of that half (NV/2 + NV/4
-// + NV/8 + NV/16 shuffles instead of 6*NV), then a plain butterfly over offsets
-// 2, 1 on the last NV/16.  Lanes with (lane & 3) == 0 then hold the wave totals;
-// the NW waves are combined in LDS in a fixed pairwise tree.  On return thread t < NV of the
-// block can read total t from out_lds[t].  Fixed order -> bitwise reproducible.
-// ---------------------------------------------------------------------------
 #ifndef ADMM_RS_DPP
-#define ADMM_RS_DPP 1  // reduce-scatter by gfx950 permlane swaps + DPP (0: __shfl_xor / ds_bpermute)
+#define ADMM_RS_DPP 1  // wave reductions by gfx950 permlane swaps + DPP (0: __shfl_xor / ds_bpermute)
 #endif
 // float64 lane exchange by DPP (two 32-bit moves); CTRL must describe an exact xor pairing
 template <int CTRL>
@@ -181,7 +150,59 @@ __device__ __forceinline__ void permswap_d(double& x, double& y) {
   x = __builtin_bit_cast(double, ((uint64_t)xh << 32) | xl);
   y = __builtin_bit_cast(double, ((uint64_t)yh << 32) | yl);
 }
+// s + (s of lane ^ 32, 16, 8, 4, 2, 1): every lane ends with the wave total, the same sums in
+// the same order as the __shfl_xor butterfly (a + b == b + a), without LDS round trips
+__device__ __forceinline__ double wave_sum_d(double s) {
+  const int lane = threadIdx.x & 63;
+  double x = s, y = s;
+  permswap_d<true>(x, y);  // x + y = s[i] + s[i ^ 32] in every lane
+  s = x + y;
+  x = s, y = s;
+  permswap_d<false>(x, y);
+  s = x + y;
+  s += dpp_d<0x128>(s);  // row_ror:8 = xor 8
+  const double up = dpp_d<0x104>(s), dn = dpp_d<0x114>(s);  // xor 4: row_shl:4 / row_shr:4
+  s += (lane & 4) ? dn : up;
+  s += dpp_d<0x4E>(s);  // quad_perm [2,3,0,1]
+  s += dpp_d<0xB1>(s);  // quad_perm [1,0,3,2]
+  return s;
+}
 
+template <int NQ>
+__device__ __forceinline__ void block_reduce(double (&v)[NQ], double* lds /* >= 4*NQ */) {
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    double s = v[q];
+    if constexpr (ADMM_RS_DPP) {
+      s = wave_sum_d(s);
+    } else {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+    }
+    v[q] = s;
+  }
+  const int wid = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) lds[wid * NQ + q] = v[q];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) v[q] = ((lds[q] + lds[NQ + q]) + (lds[2 * NQ + q] + lds[3 * NQ + q]));
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// deterministic block reduction of NV (multiple of 16) float64 values per thread
+// by a wave-level reduce-scatter butterfly: at offsets 32, 16, 8, 4 every lane
+// keeps half of its values and adds its partner's copy of that half (NV/2 + NV/4
+// + NV/8 + NV/16 shuffles instead of 6*NV), then a plain butterfly over offsets
+// 2, 1 on the last NV/16.  Lanes with (lane & 3) == 0 then hold the wave totals;
+// the NW waves are combined in LDS in a fixed pairwise tree.  On return thread t < NV of the
+// block can read total t from out_lds[t].  Fixed order -> bitwise reproducible.
+// ---------------------------------------------------------------------------
 template <int NV, int NW = 4>
 __device__ __forceinline__ void block_reduce_rs(double (&v)[NV], double* lds /* >= NW*NV */,
                                                 double* out_lds /* >= NV */) {
