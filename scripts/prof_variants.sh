@@ -4,7 +4,7 @@ set -u
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 for v in "$@"; do
   ADMM_TOMO_LIB=variants/lib_$v.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profv_$v -o run \
-    --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/profv_$v.log 2>&1 || exit $?
+    --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --strong none > gpurun_out/profv_$v.log 2>&1 || exit $?
   f=$(find gpurun_out/profv_$v -name "*kernel_stats.csv" | head -1)
   python - "$f" "$v" <<'PY'
 import csv, sys
