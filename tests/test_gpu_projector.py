@@ -56,7 +56,8 @@ def test_adjoint_matches_oracle(cuda, N, a, dtype):
         assert rel(X[v], joseph_adjoint_gather(Geometry(N, a), Ys[v])) < TOL[dtype]
 
 
-@pytest.mark.parametrize("N,a", [(16, 12), (64, 45), (128, 96)])
+# N = 2: L = 2/(N max(|cos|, |sin|)) > 1, so the float weights run scaled by 2^-wexp (k_back)
+@pytest.mark.parametrize("N,a", [(2, 3), (3, 5), (16, 12), (64, 45), (128, 96)])
 def test_column_norms_match_oracle(cuda, N, a):
     A = joseph_matrix(Geometry(N, a))
     W = np.maximum(np.asarray(A.multiply(A).sum(axis=0)).ravel(), 1e-12)
@@ -74,15 +75,19 @@ def test_numpy_roundtrip_and_batch_of_one(cuda):
     assert (op.T @ y).shape == (32 * 32,)
 
 
-def test_detector_wider_than_image(cuda):
-    """det_width_factor > 1 (block_2_load_odl_data.py:16,42): rays outside the image are 0."""
+@pytest.mark.parametrize("dtype", ["float32", "float64"])
+def test_detector_wider_than_image(cuda, dtype):
+    """det_width_factor > 1 (block_2_load_odl_data.py:16,42): rays outside the image are 0
+    (every k_f of the back projector is positive without a bias here)."""
     g = Geometry(40, 30, det_width_factor=1.5)
     A = joseph_matrix(g)
-    op = RayTransform(ParallelBeamGeometry(40, 30, det_width_factor=1.5), "float64")
-    x = np.random.default_rng(3).standard_normal(1600)
-    assert rel(op @ x, A @ x) < 1e-12
-    y = np.random.default_rng(4).standard_normal(A.shape[0])
-    assert rel(op.T @ y, A.T @ y) < 1e-12
+    op = RayTransform(ParallelBeamGeometry(40, 30, det_width_factor=1.5), dtype)
+    tdt = torch.float64 if dtype == "float64" else torch.float32
+    x = torch.as_tensor(np.random.default_rng(3).standard_normal(1600), dtype=tdt)
+    y = torch.as_tensor(np.random.default_rng(4).standard_normal(A.shape[0]), dtype=tdt)
+    xs, ys = x.double().numpy(), y.double().numpy()
+    assert rel((op @ x.to(cuda)).double().cpu().numpy(), A @ xs) < TOL[dtype]
+    assert rel((op.T @ y.to(cuda)).double().cpu().numpy(), A.T @ ys) < TOL[dtype]
 
 
 def test_finer_detector_rejected(cuda):
