@@ -17,8 +17,9 @@ from oracle.geometry import Geometry, joseph_matrix, shepp_logan, joseph_adjoint
 pytestmark = pytest.mark.gpu
 
 # (N, angles): 45 angles put one midpoint exactly at pi/2 (cos = 6e-17, dl ~ 0);
-# 48 and 37 are non-multiples of the 64-wide tiles; 2 is the smallest image.
-CASES = [(2, 3), (16, 12), (37, 19), (48, 36), (64, 48), (64, 45), (128, 96)]
+# 48 and 37 are non-multiples of the 64-wide tiles; 2 is the smallest image; 150 angles take
+# the back projector past one 96-angle window chunk.
+CASES = [(2, 3), (16, 12), (37, 19), (48, 36), (64, 48), (64, 45), (128, 96), (64, 150)]
 TOL = {"float32": 2e-6, "float64": 1e-12}
 
 
