@@ -13,6 +13,11 @@ residual/statistics readback the reference's stop test needs.
     python bench.py --config C2|C3|C4|C5|C5s   (BASELINE.json configs[1..4], fixed node count,
                                                  sharded over however many ranks run it)
 
+``python bench.py --gpus N`` with N > 1 and no WORLD_SIZE in the environment launches
+the N ranks itself (one child process per GPU, RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR=127.0.0.1 / MASTER_PORT set; the parent makes no GPU call), relays rank 0's
+line and exits non-zero if any rank fails.  Under a launcher, --gpus must equal WORLD_SIZE.
+
 Rank 0 prints one JSON line.  Besides the weak-scaling headline, the line carries a
 strong-scaling measurement (``strong``: BASELINE configs[3], C4 = 1024^2 / 32-node
 Erdos-Renyi graph, fixed total work, sharded over the same N ranks), so one driver
@@ -31,7 +36,8 @@ taps and so exceeds any memory peak -- it is reported as a reuse factor, not a r
 CPU baseline (``cpu_baseline``): the float64 NumPy/SciPy oracle (oracle/, the port of
 the reference algorithm -- the reference's CVXPY/ODL path cannot run here) doing the
 SAME first x-update of node 0 (the GPU's own float32 sinogram, precisions and zero
-start) in one process per host core; ``rel_fro`` = GPU node-0 image vs that oracle image.
+start) in one process per host core; ``rel_fro`` = GPU node-0 image vs that oracle image;
+``eq1_gap`` = that image's certified distance from eq.(1)'s exact minimiser (oracle/eq1.py).
 """
 from __future__ import annotations
 
@@ -114,17 +120,28 @@ def _cpu_worker(wid, N, a, b, q, budget, barrier, out):
     prm = ons.NodeParams(rho=RHO, lam=LAM, mu=10 * LAM, tv_iters=TV_ITERS, cg_iters=CG_ITERS)
     barrier.wait()
     t0 = time.perf_counter()
-    done, x = 0, None
+    done, x, st0 = 0, None, None
     while True:
         st = ons.NodeState.zeros(n)
         ons.node_update(A, Atb, b, 2 * q, 2 * q * v, [(q, v), (q, v)], st, N, prm, AT=AT)
         done += 1
         el = time.perf_counter() - t0
         if x is None:
-            x = st.x
+            x, st0 = st.x, st
         if el >= budget:
             break
-    out.put((wid, done, el, x if wid == 0 else None))
+    cert = None
+    if wid == 0:
+        # eq.(1)'s optimality certificate for the oracle image (after the timed region): with
+        # the split-Bregman dual p = mu e / lam and m = rho min(D) <= lambda_min(H),
+        # ||x - x*|| <= (||r|| + sqrt(||r||^2 + 2 m eps)) / m  (oracle/eq1.py)
+        from oracle import eq1
+        D = 2 * q
+        delta, gap, rn, eps = eq1.certificate(A, b, D, 2 * q * v, st0.x, prm.mu * st0.ex / prm.lam,
+                                              prm.mu * st0.ey / prm.lam, N, prm.rho, prm.lam, "iso")
+        cert = dict(dist_bound=delta, rel_dist_bound=delta / float(np.linalg.norm(st0.x)), obj_gap_bound=gap,
+                    stationarity=rn, eps=eps, m=float(prm.rho * D.min()))
+    out.put((wid, done, el, x if wid == 0 else None, cert))
 
 
 def cpu_baseline(N, a, b, q, x_gpu, procs=None, budget=CPU_BASELINE_SECONDS):
@@ -163,9 +180,16 @@ def cpu_baseline(N, a, b, q, x_gpu, procs=None, budget=CPU_BASELINE_SECONDS):
     done = sum(r[1] for r in res)
     el = max(r[2] for r in res)
     x_cpu = next(r[3] for r in res if r[0] == 0)
+    cert = next(r[4] for r in res if r[0] == 0)
     rel = float(np.linalg.norm(x_gpu - x_cpu) / np.linalg.norm(x_cpu))
     return {"value": done / el, "unit": "node-updates/s", "cores": procs, "kind": "port",
             "rel_fro": rel,
+            "eq1_gap": dict(cert, note="certified distance of the oracle's node-0 image (the iteration the "
+                                       "GPU matches to rel_fro) from eq.(1)'s exact minimiser "
+                                       "(block_5_node_problem.py:21-29): split-Bregman dual p = mu e / lam, "
+                                       "strong convexity m = rho min(D) (a lower bound on lambda_min(H)); "
+                                       "obj_gap_bound = ||r||^2 / 2m + eps >= f(x) - f(x*); the reference's "
+                                       "SCS solve is inexact too (eps = min(1e-2, eps_target))"),
             "sample": f"{done} x-updates of node 0's first ADMM iteration ({N}^2, {a} angles, 2 ring "
                       f"neighbours, 10x5 inner, zero start) on the GPU run's own float32 sinogram "
                       f"and precisions; float64 SciPy CSR Joseph oracle, {procs} processes x 1 "
@@ -269,6 +293,41 @@ def timed_steps(r, steps, warmup, world, prime=None):
     return el
 
 
+def launch_ranks(n: int) -> int:
+    """Run this script as ``n`` rank processes (one per GPU) and return the exit status.
+
+    The parent has not touched the GPU (no torch import): children are started fresh with
+    the torch.distributed env contract; rank 0 prints the JSON line to the shared stdout.
+    If a rank fails the others are terminated (a peer blocked in a collective would hang)."""
+    import signal
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 1
+                print(f"bench: rank {procs.index(p)} exited with {rc}; stopping the others", file=sys.stderr)
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.2)
+    return status
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -282,16 +341,19 @@ def main():
                     help="strong-scaling config measured after the headline ('none' to skip)")
     ap.add_argument("--strong-steps", type=int, default=3)
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))  # decided before any GPU call of this process
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        ap.error(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU, they must match")
 
-    import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     # one process per GPU; ADMM_DIST_BACKEND=gloo (+ more ranks than GPUs) is a 1-GPU
     # rehearsal of the sharded path only -- the measured configuration is nccl (RCCL)
     backend = os.environ.get("ADMM_DIST_BACKEND", "nccl")

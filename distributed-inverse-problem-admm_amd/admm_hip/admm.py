@@ -21,7 +21,10 @@ x-updates until its split-Bregman residual <= eps_try, at most ``max_inner_updat
 solve, standing in for SCS's tolerance), accepted if the reference's ||g|| <= eps_target,
 else eps_try /= 5 and re-solved, at most twice, then force-accepted; eps_used is the
 eps_try of the accepted iterate.  Other nodes' state is untouched while one node
-re-solves (masked batch updates).  One process per GPU: when
+re-solves (masked batch updates).  Nodes may have different operators (the reference's
+own angle split gives unequal counts, block_2_load_odl_data.py:31-38; matrix lists may
+hold any matrices): each distinct operator is one device batch (groups.RankGroups).
+One process per GPU: when
 ``torch.distributed`` is initialised with world size > 1 the graph nodes are
 sharded (plan.py) and every rank returns the same ``(x_list, history)``.
 """
@@ -35,11 +38,9 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from .exchange import HaloExchange, assemble_stats, gather_images
 from .geometry import RayTransform
+from .groups import RankGroups
 from .matrix import MatrixOperator, as_operators
-from .plan import make_plan
-from .solver import NodeBatch
 
 HISTORY_KEYS = (
     "primal", "dual", "pri_per_node", "dual_per_node", "obj_per_node", "obj_total",
@@ -58,8 +59,9 @@ def eps_target(k: int) -> float:
     return 2.0 / ((k + 1) ** 1.005)
 
 
-def _common_geometry(A_list):
-    geoms = set()
+def _check_operators(A_list, N):
+    """Every entry an admm_hip operator on an N x N image.  Nodes may have different
+    operators (unequal angle counts, different matrices): RankGroups batches equal ones."""
     for A in A_list:
         if not isinstance(A, (RayTransform, MatrixOperator)):
             raise TypeError(
@@ -67,13 +69,8 @@ def _common_geometry(A_list):
                 f"or matrices; got {type(A).__name__}")
         if A._adjoint:
             raise ValueError("A_dense_list entry is an adjoint view")
-        geoms.add((A.geom, A.dtype, A.device))
-    if len(geoms) != 1:
-        raise NotImplementedError(
-            "all nodes must share one operator (same geometry / same matrix): the batched "
-            "kernels project every node with one angle table or one CSR matrix; choose "
-            "angles_total divisible by num_nodes")
-    return geoms.pop()
+        if A.geom.N != N:
+            raise ValueError(f"N={N} does not match an operator's N={A.geom.N}")
 
 
 def _dist_info(group):
@@ -87,10 +84,12 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
              snapshot_every=None, snapshot_div=10, phantom_true=None, mu=None, tv_iters=10,
              cg_iters=5, tv_kind="iso", group=None, return_tensors=False, timing=None,
              write_params=True, fusion="midpoint", inner_tol=None, max_inner_updates=10,
-             inner_chunks=None, chunk_snapshot_dir=None, chunk_save_every=1):
+             inner_chunks=None, chunk_snapshot_dir=None, chunk_save_every=1, inspect=None):
     """``inner_chunks``: split each x-update into warm-started solves of these round counts
     (block_6_admm_loop.py:14-69 chunked SCS); ``chunk_snapshot_dir`` then receives that
-    file's per-chunk snapshots (``_chunk_snapshot``) every ``chunk_save_every`` chunks."""
+    file's per-chunk snapshots (``_chunk_snapshot``) every ``chunk_save_every`` chunks.
+    ``inspect(rg)``: called with the rank's device state (groups.RankGroups) after the loop
+    (tests check the edge invariants on the device arrays)."""
     if inner_tol not in (None, "reference"):
         raise ValueError("inner_tol must be None (fixed counts) or 'reference'")
     if inner_chunks is not None:
@@ -104,26 +103,23 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
     # matrices (the reference's dense A_dense_list; dense numpy / torch, scipy.sparse)
     # become explicit-matrix operators (matrix.py); operators pass through
     A_dense_list = as_operators(A_dense_list, N=N)
-    geom, dtype, device = _common_geometry(A_dense_list)
-    if geom.N != N:
-        raise ValueError(f"N={N} does not match the operators' N={geom.N}")
+    _check_operators(A_dense_list, N)
     if sorted(G.nodes()) != list(range(V_total)):
         raise ValueError("graph nodes must be 0..num_nodes-1")
     mu = DEFAULT_MU_FACTOR * lam_tv if mu is None else float(mu)
     if not mu > 0:
         raise ValueError("mu must be > 0 (set lam_tv > 0 or pass mu explicitly)")
     world, rank = _dist_info(group)
-    torch.cuda.set_device(device)
-    plan = make_plan(G, V_total, world, rank)
+    torch.cuda.set_device(A_dense_list[0].device)
     if snapshot_dir is not None:
         os.makedirs(snapshot_dir, exist_ok=True)
     if snapshot_every is None:
         snapshot_every = max(1, max_iters // snapshot_div)  # _ver2:31-32
-    nb = NodeBatch(geom, dtype, plan, sinograms, Qij_diag_fn, rho, lam_tv, mu, tv_iters, cg_iters,
-                   tv_kind, phantom_true, device, fusion=fusion, Wi_list=Wi_list,
-                   keep_x=inner_tol is None)  # this loop never writes x itself (masked
-    # re-solves of the tolerance mode restore x rows, so that mode re-projects x)
-    halo = HaloExchange(plan, nb.x_ext, group)
+    rg = RankGroups(A_dense_list, G, V_total, world, rank, sinograms, Qij_diag_fn, rho, lam_tv, mu,
+                    tv_iters, cg_iters, tv_kind, phantom_true, fusion=fusion, Wi_list=Wi_list,
+                    keep_x=inner_tol is None, group=group)  # this loop never writes x itself
+    # (masked re-solves of the tolerance mode restore x rows, so that mode re-projects x)
+    plan = rg.plan
     if world > 1:
         dist.barrier(group=group)
     hist = {k: [] for k in HISTORY_KEYS + EXTRA_KEYS}
@@ -140,22 +136,21 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
     for k in range(max_iters):
         et = eps_target(k)
         if inner_chunks is None:
-            nb.node_update()
+            rg.node_update()
         else:
             for cid, rounds in enumerate(inner_chunks):
-                nb.node_update(rounds=rounds)
+                rg.node_update(rounds=rounds)
                 if chunk_snapshot_dir is not None and cid % int(chunk_save_every) == 0:
-                    _chunk_snapshot(chunk_snapshot_dir, k, cid, plan, nb.x_local, N)
+                    _chunk_snapshot(chunk_snapshot_dir, k, cid, rg, N)
         eps_used = np.full(plan.V, np.nan)
         n_upd = np.ones(plan.V)
         if inner_tol == "reference":
-            eps_used, n_upd = _solve_to_reference_tolerance(nb, et, max_inner_updates)
-        halo.run()
-        nb.consensus()
-        extra = torch.as_tensor(np.stack([eps_used, n_upd], axis=1), dtype=torch.float64,
-                                device=nb.node_stats.device)
-        ns, es = assemble_stats(plan, torch.cat([nb.node_stats, extra], dim=1),
-                                nb.edge_stats[: len(plan.stored_edges)], group)
+            for nb in rg.batches:
+                rows = [plan.local_nodes.index(g) for g in nb.plan.local_nodes]
+                eps_used[rows], n_upd[rows] = _solve_to_reference_tolerance(nb, et, max_inner_updates)
+        rg.exchange()
+        rg.consensus()
+        ns, es = rg.stats(np.stack([eps_used, n_upd], axis=1))
         ns = ns.numpy()
         es = es.numpy()
         iters_done = k + 1
@@ -194,7 +189,7 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
         hist["pri_per_node"].append(np.sqrt(pri))
         hist["dual_per_node"].append(np.sqrt(dua))
         if snapshot_dir is not None and ((k + 1) % snapshot_every == 0):
-            _snapshot(snapshot_dir, k, plan, nb.x_local, N)
+            _snapshot(snapshot_dir, k, rg, N)
         if verbose and rank == 0 and k % 10 == 0:
             print(f"iter {k}, primal {pn:.3e}, dual {dn:.3e}")
         if pn < eps_pri and dn < eps_dual:
@@ -209,7 +204,9 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
         timing["V_total"] = V_total
     if write_params and rank == 0:
         _write_params(snapshot_dir, rho, lam_tv, V_total, mu, tv_iters, cg_iters)
-    X = gather_images(plan, nb.x_local, group)
+    if inspect is not None:
+        inspect(rg)
+    X = rg.images()
     if return_tensors:
         return [X[i] for i in range(V_total)], hist
     Xh = X.to("cpu").numpy()
@@ -241,16 +238,15 @@ def _solve_to_reference_tolerance(nb, et, max_inner_updates):
         eps_try[active] /= 5.0  # :174-176
 
 
-def _chunk_snapshot(out_dir, k, cid, plan, x_local, N):
+def _chunk_snapshot(out_dir, k, cid, rg, N):
     """block_6_admm_loop.py:55-66: {out_dir}/node_{i}/node_{i}_outer_{k}_chunk_{c}.npy holding
     x.reshape(N, N, order="F") (the skeleton's Fortran-order image), + .png."""
-    xs = x_local.to("cpu").numpy()
     plt = _pyplot()
-    for r, g in enumerate(plan.local_nodes):
+    for g, xr in rg.local_images():
         d = os.path.join(out_dir, f"node_{g}")
         os.makedirs(d, exist_ok=True)
         tag = f"node_{g}_outer_{k}"
-        img = xs[r].reshape(N, N, order="F")
+        img = xr.to("cpu").numpy().reshape(N, N, order="F")
         np.save(os.path.join(d, f"{tag}_chunk_{cid}.npy"), img)
         if plt is not None:
             plt.figure(figsize=(5, 5))
@@ -272,13 +268,12 @@ def _pyplot():
         return None
 
 
-def _snapshot(snapshot_dir, k, plan, x_local, N):
+def _snapshot(snapshot_dir, k, rg, N):
     """_ver2:269-281: iter_XXXX_node_i.npy (C-order reshape) + .png."""
     it_tag = f"iter_{k + 1:04d}"
-    xs = x_local.to("cpu").numpy()
     plt = _pyplot()
-    for r, g in enumerate(plan.local_nodes):
-        img = xs[r].reshape(N, N)
+    for g, xr in rg.local_images():
+        img = xr.to("cpu").numpy().reshape(N, N)
         np.save(os.path.join(snapshot_dir, f"{it_tag}_node_{g}.npy"), img)
         if plt is not None:
             plt.figure(figsize=(5, 5))

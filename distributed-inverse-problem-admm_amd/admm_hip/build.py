@@ -39,7 +39,13 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None,
     arch = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
     tmp = target + ".tmp"
     dflags = [f"-D{k}={v}" for k, v in (defines or {}).items()]
-    cmd = [hipcc(), f"--offload-arch={arch}", "-O3", "-std=c++17", "-fPIC", "-shared",
+    # -ffp-contract=off: no compiler-formed fmas.  Contraction is decided per template
+    # instantiation, so with it the same expression could round differently for batch widths
+    # VB = 1 and VB = 4 (measured: k_fwd_combine<float, 1, 1> fused Ax*L - b into one fma,
+    # <float, 4, 1> did not), and a node's result would depend on how many nodes share its
+    # batch -- i.e. on the GPU count and on the operator groups.  Every fma the kernels
+    # rely on is written explicitly (fma(), v_pk_fma asm).
+    cmd = [hipcc(), f"--offload-arch={arch}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
            "-Wall", "-Wno-unused-function", *dflags, "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

@@ -63,8 +63,42 @@ def make_sinograms(ops: list[RayTransform], phantom, noise_level: float = 0.005,
         gen.manual_seed(seed + i)
         noise = torch.randn(clean.shape, generator=gen, device=dev, dtype=torch.float64)
         b = (clean.to(torch.float64) + noise_level * noise).to(clean.dtype)
-        out.append(b.reshape(A.geom.n_angles, A.geom.n_det))
+        # (angles, detector bins) like the reference's sinograms; a matrix operator's rows flat
+        out.append(b.reshape(-1) if hasattr(A.geom, "digest") else b.reshape(A.geom.n_angles, A.geom.n_det))
     return out
+
+
+def ridge_ls(A, b, lam_ridge: float = 1e-3, max_iters: int = 2000, rtol: float = 1e-10):
+    """argmin_x ||A x - b||^2 + lam_ridge ||x||^2 = (A^T A + lam I)^{-1} A^T b, by CG on the GPU.
+
+    The legacy loader's aggregate reconstruction (/root/reference/block_2_test.py:83-88:
+    ``np.linalg.solve(A_agg.T @ A_agg + 1e-3 I, A_agg.T @ b)`` on the dense n x n normal
+    matrix).  The normal operator is applied matrix-free with float64 samples (a float32
+    projector's rounding, amplified by the ridge system's conditioning, would show at the
+    1e-4 level); stops when ||r|| <= rtol ||A^T b|| or after ``max_iters`` steps.
+    Returns (x float64 (n,) tensor, iterations, relative residual)."""
+    from .geometry import RayTransform
+    Af = RayTransform(A.geom, "float64", A.device) if isinstance(A, RayTransform) else A
+    dev = torch.device("cuda", Af.device)
+    bt = torch.as_tensor(b).reshape(-1).to(device=dev, dtype=torch.float64)
+    atb = Af.T @ bt
+    x = torch.zeros_like(atb)
+    r = atb.clone()
+    p = r.clone()
+    rs = float(r @ r)
+    stop = (rtol ** 2) * rs
+    it = 0
+    while it < max_iters and rs > stop:
+        Ap = Af.T @ (Af @ p) + lam_ridge * p
+        alpha = rs / float(p @ Ap)
+        x += alpha * p
+        r -= alpha * Ap
+        rs_new = float(r @ r)
+        p = r + (rs_new / rs) * p
+        rs = rs_new
+        it += 1
+    base = float(atb @ atb)
+    return x, it, (rs / base) ** 0.5 if base > 0 else 0.0
 
 
 class QProvider:

@@ -104,40 +104,61 @@ def _all_reduce_sum(t: torch.Tensor, group=None) -> torch.Tensor:
 
 
 def assemble_stats(plan: ShardPlan, node_stats: torch.Tensor, edge_stats: torch.Tensor, group=None):
-    """Global (V_total, 5) node and (E_total, 3) edge statistics as float64 CPU tensors."""
-    E = len(plan.edges)
-    ns = node_stats.shape[1]
-    es = edge_stats.shape[1] if edge_stats is not None else 3
-    dev = node_stats.device
-    if plan.world == 1:
-        nodes = node_stats.detach().to("cpu")
+    """Global (V_total, ns) node and (E_total, es) edge statistics as float64 CPU tensors."""
+    return assemble_stats_parts(plan.V_total, len(plan.edges), plan.world,
+                                [(plan, node_stats, edge_stats)], group)
+
+
+def assemble_stats_parts(V_total: int, E: int, world: int, parts, group=None):
+    """Statistics of several batches (``parts`` = [(plan, node_stats, edge_stats)], one per
+    node batch of this rank) as global (V_total, ns) / (E, es) float64 CPU tensors.  Every
+    entry has exactly one writer -- the batch holding the node, the batch owning the edge
+    (lower endpoint) -- into a zero table, so the values are the writers' bits (x + 0 = x)
+    however the nodes are split over batches and ranks."""
+    plan0, ns0, es0 = parts[0]
+    ns = ns0.shape[1]
+    es = es0.shape[1] if es0 is not None else 3
+    if world == 1 and len(parts) == 1:
+        nodes = ns0.detach().to("cpu")
         edges = torch.zeros((E, es), dtype=torch.float64)
-        if E:
-            edges[torch.tensor(plan.stored_edges, dtype=torch.long)] = edge_stats.detach().to("cpu")
+        if E and plan0.stored_edges:
+            edges[torch.tensor(plan0.stored_edges, dtype=torch.long)] = es0.detach().to("cpu")
         return nodes, edges
-    buf = torch.zeros(plan.V_total * ns + E * es, dtype=torch.float64, device=dev)
-    lo = plan.local_nodes[0] if plan.local_nodes else 0
-    buf[lo * ns:(lo + plan.V) * ns].copy_(node_stats.reshape(-1))
-    owned = [k for k, o in enumerate(plan.owned_edge) if o]
-    if owned:
-        slots = torch.tensor(owned, dtype=torch.long, device=dev)
-        gids = torch.tensor([plan.stored_edges[k] for k in owned], dtype=torch.long, device=dev)
-        ev = buf[plan.V_total * ns:].view(E, es)
-        ev.index_copy_(0, gids, edge_stats.index_select(0, slots))
-    _all_reduce_sum(buf, group)
+    dev = ns0.device
+    buf = torch.zeros(V_total * ns + E * es, dtype=torch.float64, device=dev)
+    nv = buf[: V_total * ns].view(V_total, ns)
+    ev = buf[V_total * ns:].view(E, es)
+    for plan, node_stats, edge_stats in parts:
+        if plan.V:
+            nv.index_copy_(0, torch.tensor(plan.local_nodes, dtype=torch.long, device=dev), node_stats)
+        owned = [k for k, o in enumerate(plan.owned_edge) if o]
+        if owned:
+            slots = torch.tensor(owned, dtype=torch.long, device=dev)
+            gids = torch.tensor([plan.stored_edges[k] for k in owned], dtype=torch.long, device=dev)
+            ev.index_copy_(0, gids, edge_stats.index_select(0, slots))
+    if world > 1:
+        _all_reduce_sum(buf, group)
     host = buf.to("cpu")
-    return host[: plan.V_total * ns].view(plan.V_total, ns), host[plan.V_total * ns:].view(E, es)
+    return host[: V_total * ns].view(V_total, ns), host[V_total * ns:].view(E, es)
 
 
 def gather_images(plan: ShardPlan, x_local: torch.Tensor, group=None) -> torch.Tensor:
     """(V_total, n) float64 images of every node on every rank (end of the loop)."""
-    if plan.world == 1:
-        return x_local
-    n = x_local.shape[1]
-    buf = torch.zeros((plan.V_total, n), dtype=x_local.dtype, device=x_local.device)
-    lo = plan.local_nodes[0] if plan.local_nodes else 0
-    buf[lo:lo + plan.V].copy_(x_local)
-    return _all_reduce_sum(buf, group)
+    return gather_images_parts(plan.V_total, plan.world, [(plan, x_local)], group)
+
+
+def gather_images_parts(V_total: int, world: int, parts, group=None) -> torch.Tensor:
+    """``parts`` = [(plan, x_local)] of this rank's batches -> (V_total, n) images (one
+    writer per row, summed over ranks)."""
+    plan0, x0 = parts[0]
+    if world == 1 and len(parts) == 1:
+        return x0
+    n = x0.shape[1]
+    buf = torch.zeros((V_total, n), dtype=x0.dtype, device=x0.device)
+    for plan, x_local in parts:
+        if plan.V:
+            buf.index_copy_(0, torch.tensor(plan.local_nodes, dtype=torch.long, device=x0.device), x_local)
+    return _all_reduce_sum(buf, group) if world > 1 else buf
 
 
 def _row_digest(rows: torch.Tensor) -> torch.Tensor:

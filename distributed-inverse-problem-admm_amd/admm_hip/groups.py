@@ -1,0 +1,147 @@
+"""One rank's graph nodes as device batches, one batch per distinct operator.
+
+The batched kernels project every node of a batch with one angle table (or one CSR
+matrix): node-interleaved samples put the same pixel of VB nodes in one vector, so
+those nodes must share A.  The reference does not guarantee that: ``load_odl_data``
+splits ``max(180, 3N)`` angles over the nodes with the remainder going to the first
+ones (/root/reference/block_2_load_odl_data.py:31-38) -- its own defaults give
+77/77/77/77/76 angles at N=128 and 39/39/38/38/38 at N=64 with 5 nodes
+(block_7_main_ver3.py:334-335) -- and a saved ``A_dense_list`` may hold any matrices.
+
+``RankGroups`` therefore splits the rank's nodes by operator key (geometry or matrix
+digest, sample dtype, device) into node batches (``NodeBatch``, each with a subset plan,
+plan.make_subset_plan).  A group larger than one batch may hold (max_batch_nodes: 63 nodes
+at 2048^2) is split into several batches the same way.  With one batch -- every BASELINE
+config at its GPU count -- the batch IS the rank:
+its ``x_ext`` is exchanged in place and nothing else runs.  With several, an edge between
+two groups is stored by both and updated bitwise identically at both (the single-y /
+two-dual edge math is elementwise and deterministic), and each group's halo rows (other
+groups' nodes, remote nodes) are filled from one rank-level image table after the
+inter-rank exchange: local rows in, ``HaloExchange.run``, halo rows out -- device copies
+of the same bytes, so the run is bitwise the one a single batch would do if the
+operators were equal.
+"""
+from __future__ import annotations
+
+import torch
+
+from .exchange import HaloExchange, assemble_stats_parts, gather_images_parts
+from .plan import ShardPlan, make_plan, make_subset_plan
+from .solver import NodeBatch
+
+
+def operator_key(A):
+    """Nodes with equal keys share one batch (one projector context)."""
+    return (A.geom, A.dtype, A.device)
+
+
+def max_batch_nodes(geom) -> int:
+    """Most nodes one device batch may hold: the library addresses a batch's node-interleaved
+    sample buffers with 32-bit offsets (admm_batch_bind: V x max(n, m) x 8 bytes < 2^31), so
+    at 2048^2 (n = 4.2 M) a batch holds at most 63 nodes -- C5's 64 on one GPU are two
+    batches.  Rounded down to whole 8-node chunks (the widest interleave)."""
+    cap = ((1 << 31) - 1) // (8 * max(geom.n, geom.m))
+    return cap - cap % 8 if cap >= 8 else max(1, cap)
+
+
+class RankGroups:
+    def __init__(self, A_list, G, V_total: int, world: int, rank: int, sinograms, Qij_diag_fn,
+                 rho, lam, mu, tv_iters, cg_iters, tv_kind, phantom, fusion="midpoint", Wi_list=None,
+                 keep_x=False, group=None):
+        self.plan: ShardPlan = make_plan(G, V_total, world, rank)
+        self.world = world
+        self.group = group
+        keys, members = [], {}
+        for g in self.plan.local_nodes:
+            k = operator_key(A_list[g])
+            if k not in members:
+                keys.append(k)
+                members[k] = []
+            members[k].append(g)
+        # groups larger than one batch may hold are split into consecutive chunks
+        split = []
+        for k in keys:
+            cap = max_batch_nodes(k[0])
+            nodes = members.pop(k)
+            for c0 in range(0, len(nodes), cap):
+                split.append((k, c0))
+                members[(k, c0)] = nodes[c0:c0 + cap]
+        keys = split
+        devices = {k[0][2] for k in keys}
+        if len(devices) > 1:
+            raise ValueError("a rank's operators must all live on one device (got "
+                             f"{sorted(devices)}): one process per GPU")
+        if len(keys) == 1:
+            plans = [self.plan]
+        else:
+            plans = [make_subset_plan(G, V_total, members[k], world, rank, self.plan.ranges, self.plan.edges)
+                     for k in keys]
+        self.batches = []
+        for k, gp in zip(keys, plans):
+            geom, dtype, device = k[0]
+            self.batches.append(NodeBatch(geom, dtype, gp, sinograms, Qij_diag_fn, rho, lam, mu, tv_iters,
+                                          cg_iters, tv_kind, phantom, device, fusion=fusion, Wi_list=Wi_list,
+                                          keep_x=keep_x))
+        self.device = self.batches[0].dev
+        if len(self.batches) == 1:
+            self.x_rank = self.batches[0].x_ext
+            self.moves = []
+        else:
+            n = self.batches[0].x_ext.shape[1]
+            self.x_rank = torch.zeros((self.plan.n_xext, n), dtype=torch.float64, device=self.device)
+            row = self.plan.xrow
+            lt = lambda v: torch.tensor(v, dtype=torch.long, device=self.device)  # noqa: E731
+            # (batch, its local rows' slots in x_rank, x_rank slots of its halo rows)
+            self.moves = [(nb, lt([row[g] for g in nb.plan.local_nodes]), lt([row[g] for g in nb.plan.halo_nodes]))
+                          for nb in self.batches]
+        self.halo = HaloExchange(self.plan, self.x_rank, group)
+
+    @property
+    def single(self) -> bool:
+        return len(self.batches) == 1
+
+    @property
+    def V(self) -> int:
+        return self.plan.V
+
+    def node_update(self, rounds: int | None = None) -> None:
+        for nb in self.batches:
+            nb.node_update(rounds)
+
+    def exchange(self) -> None:
+        """Every batch's halo rows <- the current images of their nodes (other batches of
+        this rank, other ranks)."""
+        for nb, loc, _ in self.moves:
+            self.x_rank.index_copy_(0, loc, nb.x_local)
+        self.halo.run()
+        for nb, _, hal in self.moves:
+            if hal.numel():
+                torch.index_select(self.x_rank, 0, hal, out=nb.x_ext[nb.V:])
+
+    def consensus(self) -> None:
+        for nb in self.batches:
+            nb.consensus()
+
+    def stats(self, extra=None):
+        """Global node / edge statistics; ``extra`` (rank-local [V, k] numpy, rows in
+        plan.local_nodes order) is appended to the node statistics."""
+        parts = []
+        for nb in self.batches:
+            ns = nb.node_stats
+            if extra is not None:
+                rows = [self.plan.local_nodes.index(g) for g in nb.plan.local_nodes]
+                ex = torch.as_tensor(extra[rows], dtype=torch.float64, device=ns.device)
+                ns = torch.cat([ns, ex], dim=1)
+            parts.append((nb.plan, ns, nb.edge_stats[: len(nb.plan.stored_edges)]))
+        return assemble_stats_parts(self.plan.V_total, len(self.plan.edges), self.world, parts, self.group)
+
+    def local_images(self):
+        """[(global node, image row tensor)] of this rank's nodes, ascending."""
+        out = []
+        for nb in self.batches:
+            out.extend((g, nb.x_local[r]) for r, g in enumerate(nb.plan.local_nodes))
+        return sorted(out, key=lambda t: t[0])
+
+    def images(self) -> torch.Tensor:
+        return gather_images_parts(self.plan.V_total, self.world,
+                                   [(nb.plan, nb.x_local) for nb in self.batches], self.group)

@@ -72,6 +72,14 @@ class MatrixGeometry:
             h.update(np.ascontiguousarray(a).tobytes())
         self.digest = h.hexdigest()
 
+    # the C context's one-"angle" layout (admm_ctx_create_matrix: n_det = m): a sinogram of a
+    # matrix operator is its m rows (make_sinograms returns it flat)
+    n_angles = 1
+
+    @property
+    def n_det(self) -> int:
+        return self.m
+
     def __eq__(self, other):
         return isinstance(other, MatrixGeometry) and other.digest == self.digest
 

@@ -2,7 +2,9 @@
 
 Pure host logic (no GPU), exercised by the world-size-2 gloo tests.
 
-* Nodes are split into contiguous blocks, one per rank.
+* Nodes are split into contiguous blocks, one per rank; within a rank,
+  nodes whose operators differ (unequal angle counts, different matrices) form separate
+  batches, each with a subset plan (``make_subset_plan``; admm_hip/groups.py).
 * Edges are the reference's ``G.edges()`` in order, canonicalised to
   (min, max) (block_6_admm_loop_ver2.py:39-43,211-212).  A rank stores every
   edge incident to one of its nodes; an edge whose endpoints live on two ranks
@@ -73,7 +75,8 @@ class ShardPlan:
         return remote > 0 and len(self.halo_nodes) * 2 > remote
 
 
-def make_plan(G, V_total: int, world: int = 1, rank: int = 0) -> ShardPlan:
+def canonical_edges(G, V_total: int) -> list:
+    """``G.edges()`` as (min, max) pairs in order, validated (block_6_admm_loop_ver2.py:39-43)."""
     edges = [(min(i, j), max(i, j)) for i, j in G.edges()]
     if len(set(edges)) != len(edges):
         raise ValueError("graph has duplicate edges")
@@ -82,10 +85,20 @@ def make_plan(G, V_total: int, world: int = 1, rank: int = 0) -> ShardPlan:
             raise ValueError("self loops are not supported")
         if not (0 <= a < V_total and 0 <= b < V_total):
             raise ValueError("edge endpoint out of range")
-    ranges = node_ranges(V_total, world)
-    lo, hi = ranges[rank]
-    P = ShardPlan(V_total=V_total, world=world, rank=rank, edges=edges, ranges=ranges)
-    P.local_nodes = list(range(lo, hi))
+    return edges
+
+
+def make_subset_plan(G, V_total: int, nodes, world: int = 1, rank: int = 0, ranges=None,
+                     edges=None) -> ShardPlan:
+    """Plan of an arbitrary set of graph nodes held by one batch: its local rows (``nodes``
+    in ascending order), the halo rows of every neighbour outside the set, the stored edges
+    (every edge incident to the set) and the incidence lists.  An edge is owned (its
+    statistics reported) by the batch holding its lower endpoint."""
+    if edges is None:
+        edges = canonical_edges(G, V_total)
+    P = ShardPlan(V_total=V_total, world=world, rank=rank, edges=edges,
+                  ranges=ranges if ranges is not None else [(0, V_total)])
+    P.local_nodes = sorted(int(g) for g in nodes)
     local = set(P.local_nodes)
     halo = set()
     for a, b in edges:
@@ -103,7 +116,7 @@ def make_plan(G, V_total: int, world: int = 1, rank: int = 0) -> ShardPlan:
             P.stored_edges.append(ge)
             P.edge_a_row.append(P.xrow[a])
             P.edge_b_row.append(P.xrow[b])
-            P.owned_edge.append(owner_of(ranges, a) == rank)
+            P.owned_edge.append(a in local)
     edge_of = {e: ge for ge, e in enumerate(edges)}
     P.inc_off = [0]
     for g in P.local_nodes:
@@ -113,6 +126,17 @@ def make_plan(G, V_total: int, world: int = 1, rank: int = 0) -> ShardPlan:
             P.inc_nbr.append(int(j))
             P.inc_sign.append(1 if g == e[0] else -1)
         P.inc_off.append(len(P.inc_edge))
+    return P
+
+
+def make_plan(G, V_total: int, world: int = 1, rank: int = 0) -> ShardPlan:
+    """Plan of rank ``rank``: the contiguous node block node_ranges(V_total, world)[rank],
+    plus which boundary images it sends to / receives from every peer."""
+    edges = canonical_edges(G, V_total)
+    ranges = node_ranges(V_total, world)
+    lo, hi = ranges[rank]
+    P = make_subset_plan(G, V_total, range(lo, hi), world, rank, ranges, edges)
+    local = set(P.local_nodes)
     for peer in range(world):
         if peer == rank:
             continue

@@ -6,10 +6,11 @@
   masks from one HIP launch (admm_hip.masks) and the masked Q_ij provider.
 
 Deviation: the reference loads a pickled list of dense matrices from
-``base_dir/A_dense_list_pickle`` (:289-295).  Pickles are not unpickled here: the
-list is read from ``.npy`` / ``.npz`` files (``admm_hip.matrix.load_matrix_list``,
-allow_pickle=False) when ``A_dense_list_pickle`` names one, else pass ``ops=`` (the
-RayTransform list of ``load_odl_data``, or matrices) or ``Wi_list=``.  Dense A is
+``base_dir/A_dense_list_pickle`` (:283-287).  Pickles are not unpickled here: the operators
+come from the descriptor ``load_odl_data`` writes into the same directory
+(``A_dense_list.json`` next to the pickle name, admm_hip/opfile.py), from ``.npy`` /
+``.npz`` matrix lists (``admm_hip.matrix.load_matrix_list``, allow_pickle=False) when
+``A_dense_list_pickle`` names one, or from ``ops=`` / ``Wi_list=``.  Dense A is
 infeasible past ~128^2.  ``keep`` comes back as a device uint8 tensor [V, V, n]
 (the reference returns a numpy bool array).
 """
@@ -32,14 +33,9 @@ def build_pixel_connected_Q_provider(base_dir="saved_operators_Incmp_Span",
     """Returns (G_union, Wi_list, Qij_diag_masked, keep) like block_3:265-319."""
     if Wi_list is None:
         if ops is None:
-            path = os.path.join(base_dir, A_dense_list_pickle)
-            if os.path.splitext(path)[1].lower() in (".npy", ".npz") and os.path.exists(path):
-                from admm_hip.matrix import as_operators, load_matrix_list
-                ops = as_operators(load_matrix_list(path), device=device)
-            else:
-                raise FileNotFoundError(
-                    f"no operators given: the reference reads {path} (pickled dense matrices, "
-                    "not unpickled here); save the list as .npy / .npz, or pass ops= or Wi_list=")
+            ops = _load_ops(base_dir, A_dense_list_pickle, device)
+            if verbose:
+                print(f"[Block3] loaded A_dense_list from {base_dir}  nodes {len(ops)}")
         Wi_list, _ = make_precisions(ops, q_mode=q_mode)
     if device is None:
         from admm_hip.geometry import default_device
@@ -50,6 +46,24 @@ def build_pixel_connected_Q_provider(base_dir="saved_operators_Incmp_Span",
         tag = f"{strategy}_k{k}_{q_mode}" if strategy == "knn" else f"{strategy}_{q_mode}"
         G_union = _summarize_union(keep, output_dir, show_plots, verbose, tag)
     return G_union, Wi_list, MaskedQProvider(Wi_list, keep, q_mode), keep
+
+
+def _load_ops(base_dir, name, device):
+    """The operator list block_2 left in ``base_dir`` (block_3:283-287 reads the pickle):
+    its descriptor (``A_dense_list.json`` / ``.npz`` next to ``A_dense_list.pkl``,
+    admm_hip/opfile.py), or ``name`` itself when it is a ``.npy`` / ``.npz`` matrix list."""
+    from admm_hip.opfile import load_operators
+    path = os.path.join(base_dir, name)
+    ops = load_operators(base_dir, name, device)
+    if ops is not None:
+        return ops
+    if os.path.splitext(path)[1].lower() in (".npy", ".npz") and os.path.exists(path):
+        from admm_hip.matrix import as_operators, load_matrix_list
+        return as_operators(load_matrix_list(path), device=device)
+    raise FileNotFoundError(
+        f"no operators given: the reference reads {path} (pickled dense matrices, not unpickled "
+        "here); run load_odl_data with this directory (it writes the operator descriptor), save "
+        "the list as .npy / .npz, or pass ops= or Wi_list=")
 
 
 def _summarize_union(keep, output_dir, show_plots, verbose, tag):

@@ -9,7 +9,10 @@ SCS controls map onto the split-Bregman inner solve (CG steps play SCS's iterati
 as block_5_node_problem's ``max_iters`` does):
 
 * ``scs_total_iters`` -> ceil(scs_total_iters / cg_iters) rounds per x-update (unless
-  ``tv_iters`` is given explicitly);
+  ``tv_iters`` is given explicitly).  The exchange rate is one CG step (one A^T A p) per
+  SCS iteration (one KKT matvec in SCS's indirect mode): a modelling choice, not an
+  equivalence.  At this file's default (100) that is 20 rounds x 5 CG steps, twice the
+  inner work of the ``_ver2`` drop-in's fixed 10 x 5 (DESIGN.md section 4);
 * ``scs_chunk_iters`` -> the x-update runs as warm-started chunks of
   ceil(scs_chunk_iters / cg_iters) rounds (:127-146, _scs_solve_in_chunks :14-69);
 * ``scs_snapshot_dir`` / ``scs_save_every_chunks`` -> after chunk c (c % every == 0)

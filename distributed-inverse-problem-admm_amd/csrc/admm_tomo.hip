@@ -41,6 +41,29 @@ int fail(int code, const std::string& msg) {
 
 size_t dsize(int dtype) { return dtype == ADMM_DTYPE_F64 ? 8 : 4; }
 
+// Makes `device` current for the scope of an entry point and restores the caller's device
+// on every return path (the operator API is called freely from Python: applying an
+// operator that lives on another GPU must not change torch.cuda.current_device()).
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int device) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != device) err = hipSetDevice(device);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
+#define DEVICE_SCOPE(dev)                                                                     \
+  DeviceGuard _dg(dev);                                                                       \
+  if (_dg.err != hipSuccess)                                                                  \
+  return fail(ADMM_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(_dg.err))
+
 struct Buf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -105,8 +128,8 @@ struct admm_ctx {
   int vb = 1;  // node interleave width of the sample buffers
   Buf xs, xsT, p, pT, Hp, sino, bI, fpart, r, c, d2, e2;
   Buf dsumS;  // D = sum_j q_ij as interleaved samples (BACK_H epilogue)
-  Buf x2, p2; // ping-pong partners of x (local rows) and p for the fused TV update (ADMM_TV_FUSE)
-  Buf pring;  // CG direction slots 1 .. K-1 (ADMM_TV_FUSE 2; slot 0 = p, slot K = p2)
+  Buf x2, p2; // ping-pong partners of x (local rows) and p for the fused TV update
+  Buf pring;  // CG direction slots 1 .. K-1 (direction ring; slot 0 = p, slot K = p2)
   Buf ats;    // A^T (A xs - b) of the last update's final x (ADMM_BATCH_KEEP_X)
   bool ats_valid = false;  // ats matches x_ext's local rows
   hipGraph_t g_update_reuse = nullptr;
@@ -116,7 +139,6 @@ struct admm_ctx {
   int P_back = 0, P_tile = 0, P_fwd = 0, P_edge = 0;
   hipGraph_t g_update = nullptr, g_cons = nullptr;
   hipGraphExec_t x_update = nullptr, x_cons = nullptr;
-  bool use_graph = true;
 };
 
 namespace {
@@ -154,14 +176,12 @@ int build_fwd_order_into(admm_ctx* C, int pl, int nch, int cus, Buf& buf, int* n
       for (int s = 0; s < kFgSeg; ++s)
         for (int kc = 0; kc < gv[gi].nkc[s]; ++kc) v.push_back({make_int4(kc, gi, s + kFgSeg * c, 0), gv[gi].G});
   const int n = (int)v.size();
-  const char* xe = getenv("ADMM_FWD_XCD");
-  const bool xcd = !(xe && xe[0] == '0');
   auto by_weight = [](std::vector<Blk>& l, int slots) {
     std::stable_sort(l.begin(), l.end(), [](const Blk& a, const Blk& b) { return a.w > b.w; });
     const int m = (int)l.size();
     if (m <= 2 * slots && m > slots) std::reverse(l.begin() + slots, l.end());
   };
-  if (cus > 0 && xcd && cus % kXcds == 0) {
+  if (cus > 0 && cus % kXcds == 0) {
     // XCD-aware: workgroups are dealt round-robin over the 8 XCDs (id % 8), so launch
     // position p runs on XCD p % 8.  Row segment s goes to XCD s % 8: each XCD's L2 then
     // holds one band of image rows (and of the transposed copy) instead of re-fetching the
@@ -214,10 +234,6 @@ int pick_fwd_plan(admm_ctx* C, int nch, int* pl_out, int* cus_out) {
   int pl = per_cu_max(1) <= per_cu_max(0) ? 1 : 0;
   const char* f = getenv("ADMM_FWD_PLAN");
   if (f && (f[0] == '0' || f[0] == '1')) pl = f[0] - '0';
-  if (getenv("ADMM_DEBUG_PLAN"))
-    fprintf(stderr, "[admm] forward plans: unaligned %d groups %d blocks, aligned %d groups %d blocks, "
-                    "x%d chunks, %d CUs -> %s\n", C->plan_n[0], C->plan_blocks[0], C->plan_n[1],
-            C->plan_blocks[1], nch, cus, pl ? "aligned" : "unaligned");
   *pl_out = pl;
   *cus_out = cus;
   return ADMM_OK;
@@ -400,13 +416,13 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 
   double* ecur = B.e;
   double* dnxt = (double*)C->d2.p;
   double* enxt = (double*)C->e2.p;
-  // ADMM_TV_FUSE 1: the round's last CG step runs inside the TV update; 2: every x step of
-  // the round does (the CG updates leave x alone and write each new direction to its own
-  // slot of a ring, p_0 .. p_K).  The TV update reads x and the directions over its tiles'
-  // halos while writing them, so x ping-pongs (xcur -> xnxt) and the restart p = r goes to
-  // the ring's spare slot.
+  // Every x step of a round is applied by the TV update that ends it (F = 2: the CG updates
+  // leave x alone and write each new direction to its own slot of a ring, p_0 .. p_K); with
+  // more CG steps than ring slots only the round's last step is (F = 1).  The TV update reads
+  // x and the directions over its tiles' halos while writing them, so x ping-pongs
+  // (xcur -> xnxt) and the restart p = r goes to the ring's spare slot.
   const int K = B.cg_iters, Tt = rounds > 0 ? rounds : B.tv_iters;
-  const int F = !ADMM_CG_SKIP_P ? 0 : (ADMM_TV_FUSE == 2 && K <= kMaxCgRing) ? 2 : (ADMM_TV_FUSE ? 1 : 0);
+  const int F = (K <= kMaxCgRing) ? 2 : 1;
   double* xcur = B.x_ext;
   double* xnxt = (double*)C->x2.p;
   std::vector<T*> slot(K + 1, p);
@@ -442,11 +458,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 
           hipLaunchKernelGGL((k_cg_update<T, VB, true, true>), cgg, dim3(kBlock), 0, s, xcur, r, (const T*)pk, pT,
                              Hp, rk, N, V, pk);
         CHECK_LAUNCH();
-      } else if (F == 0) {  // p is overwritten next (TV update / next x-update start)
-        hipLaunchKernelGGL((k_cg_update<T, VB, false, true>), cgg, dim3(kBlock), 0, s, xcur, r, (const T*)pk, pT,
-                           Hp, rk, N, V, pk);
-        CHECK_LAUNCH();
-      }
+      }  // the round's last step: applied by the TV update
     }
     const bool last = (t + 1 == Tt);
     PRing<T> pr{};
@@ -455,47 +467,34 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 
     T* pout = last ? xs : (F == 2 ? slot[K] : (F == 1 ? slot[1] : slot[0]));
     T* poutT = last ? xsT : pT;
     // split-Bregman state in/out of this round: d, e (B.d / B.e or the scratch pair) or,
-    // between the rounds of the update (ADMM_TV_USTATE, Tt > 1), u = Kx + e in ua / ub
-    const bool uin = ADMM_TV_USTATE && t > 0 && Tt > 1;
-    const bool uout = ADMM_TV_USTATE && !last && Tt > 1;
+    // between the rounds of the update (Tt > 1), u = Kx + e in ua / ub
+    const bool uin = t > 0 && Tt > 1;
+    const bool uout = !last && Tt > 1;
     double* ua = (double*)C->d2.p;
     double* ub = (double*)C->e2.p;
     const double* din = uin ? ((t % 2) ? ua : ub) : dcur;
     const double* ein = ecur;  // (not read when uin)
-    double* dout = uout ? ((t % 2) ? ub : ua) : (ADMM_TV_USTATE && Tt > 1 ? B.d : dnxt);
-    double* eout = uout ? nullptr : (ADMM_TV_USTATE && Tt > 1 ? B.e : enxt);
+    double* dout = uout ? ((t % 2) ? ub : ua) : (Tt > 1 ? B.d : dnxt);
+    double* eout = uout ? nullptr : (Tt > 1 ? B.e : enxt);
 #define TV_LAUNCH(LASTV, FUSEV, UINV, UOUTV)                                                                     \
   hipLaunchKernelGGL((k_tv_update<T, VB, LASTV, FUSEV, UINV, UOUTV>), tg, dim3(kBlock), 0, s, xcur, din, ein, dout, \
                      eout, r, pout, poutT, tau, B.mu, B.tv_kind, N, V, xnxt, pr, Hp, redH)
-    if (F) {
-      if (!last) {
-        if (uin) TV_LAUNCH(false, true, true, true);
-        else if (uout) TV_LAUNCH(false, true, false, true);
-        else TV_LAUNCH(false, true, false, false);
-      } else {
-        if (uin) TV_LAUNCH(true, true, true, false);
-        else TV_LAUNCH(true, true, false, false);
-      }
+    if (!last) {
+      if (uin) TV_LAUNCH(false, true, true, true);
+      else if (uout) TV_LAUNCH(false, true, false, true);
+      else TV_LAUNCH(false, true, false, false);
     } else {
-      if (!last) {
-        if (uin) TV_LAUNCH(false, false, true, true);
-        else if (uout) TV_LAUNCH(false, false, false, true);
-        else TV_LAUNCH(false, false, false, false);
-      } else {
-        if (uin) TV_LAUNCH(true, false, true, false);
-        else TV_LAUNCH(true, false, false, false);
-      }
+      if (uin) TV_LAUNCH(true, true, true, false);
+      else TV_LAUNCH(true, true, false, false);
     }
 #undef TV_LAUNCH
     CHECK_LAUNCH();
-    if (!(ADMM_TV_USTATE && Tt > 1)) {
+    if (Tt == 1) {  // one round: d, e went to the scratch pair
       std::swap(dcur, dnxt);
       std::swap(ecur, enxt);
     }
-    if (F) {
-      std::swap(xcur, xnxt);
-      if (!last) std::swap(slot[0], slot[F == 2 ? K : 1]);
-    }
+    std::swap(xcur, xnxt);
+    if (!last) std::swap(slot[0], slot[F == 2 ? K : 1]);
   }
   if (xcur != B.x_ext)  // odd number of fused rounds: x ended in scratch
     HIPCHK(hipMemcpyAsync(B.x_ext, xcur, (size_t)V * npix * sizeof(double), hipMemcpyDeviceToDevice, s));
@@ -669,7 +668,7 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
   const size_t npix = (size_t)g.N * g.N, m = (size_t)g.n_angles * g.n_det;
   if ((size_t)max_images * npix * 8 >= (1ull << 31) || (size_t)max_images * m * 8 >= (1ull << 31))
     return fail(ADMM_E_INVALID, "batch too large for 32-bit buffer offsets; split it across contexts");
-  HIPCHK(hipSetDevice(device));
+  DEVICE_SCOPE(device);
   admm_ctx* C = new admm_ctx();
   C->g = g;
   C->dtype = dtype;
@@ -677,8 +676,6 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
   C->max_images = max_images;
   C->npix = (int)npix;
   C->mrays = (int)m;
-  const char* ng = getenv("ADMM_NO_GRAPH");
-  C->use_graph = !(ng && ng[0] == '1');
 
   // geometry tables, float64 (oracle/geometry.py)
   std::vector<FwdAngle> fa(g.n_angles);
@@ -791,7 +788,6 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
         t0 += G;
       }
     }
-    if (getenv("ADMM_NO_FWDG") && getenv("ADMM_NO_FWDG")[0] == '1') fits = false;
   }
   hipError_t e1 = hipMalloc(&C->fang, fa.size() * sizeof(FwdAngle));
   hipError_t e2 = hipMalloc(&C->bang, ba.size() * sizeof(BackAngle));
@@ -852,7 +848,7 @@ int admm_ctx_create_matrix(admm_ctx** out, int N, int m, long long nnz, const lo
   }
   std::vector<int> fptr(m + 1);
   for (int r = 0; r <= m; ++r) fptr[r] = (int)indptr[r];
-  HIPCHK(hipSetDevice(device));
+  DEVICE_SCOPE(device);
   admm_ctx* C = new admm_ctx();
   // a one-"angle" geometry (n_det = m, L = 1): every m-sized buffer, the fixed-order
   // reductions and the combine/residual kernels keep their shapes
@@ -867,8 +863,6 @@ int admm_ctx_create_matrix(admm_ctx** out, int N, int m, long long nnz, const lo
   C->mrays = m;
   C->csr = true;
   C->nnz = nnz;
-  const char* ng = getenv("ADMM_NO_GRAPH");
-  C->use_graph = !(ng && ng[0] == '1');
   FwdAngle fa{};
   fa.L = 1.0;
   BackAngle ba{};
@@ -912,7 +906,7 @@ int admm_ctx_create_matrix(admm_ctx** out, int N, int m, long long nnz, const lo
 
 int admm_ctx_destroy(admm_ctx* C) {
   if (!C) return ADMM_OK;
-  (void)hipSetDevice(C->device);
+  DeviceGuard _dg(C->device);
   (void)hipDeviceSynchronize();
   free_graphs(C);
   Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->op_sino, &C->op_fpart, &C->op_order[0], &C->op_order[1], &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->bI, &C->fpart, &C->r, &C->c,
@@ -934,7 +928,7 @@ int admm_project_fwd(admm_ctx* C, const void* img, void* sino, int nimg, void* s
   if (!C || !img || !sino) return fail(ADMM_E_INVALID, "null argument");
   if (nimg < 1 || nimg > C->max_images) return fail(ADMM_E_INVALID, "nimg out of range");
   hipStream_t s = (hipStream_t)stream;
-  HIPCHK(hipSetDevice(C->device));
+  DEVICE_SCOPE(C->device);
   return C->dtype == ADMM_DTYPE_F32 ? op_forward<float>(C, (const float*)img, (float*)sino, nimg, s)
                                     : op_forward<double>(C, (const double*)img, (double*)sino, nimg, s);
 }
@@ -942,6 +936,7 @@ int admm_project_fwd(admm_ctx* C, const void* img, void* sino, int nimg, void* s
 int admm_project_adj(admm_ctx* C, const void* sino, void* img, int nimg, void* stream) {
   if (!C || !img || !sino) return fail(ADMM_E_INVALID, "null argument");
   if (nimg < 1 || nimg > C->max_images) return fail(ADMM_E_INVALID, "nimg out of range");
+  DEVICE_SCOPE(C->device);
   hipStream_t s = (hipStream_t)stream;
   if (C->dtype == ADMM_DTYPE_F32) {
     BackArgs<float> a{};
@@ -957,6 +952,7 @@ int admm_project_adj(admm_ctx* C, const void* sino, void* img, int nimg, void* s
 
 int admm_column_norms_sq(admm_ctx* C, double* W, void* stream) {
   if (!C || !W) return fail(ADMM_E_INVALID, "null argument");
+  DEVICE_SCOPE(C->device);
   hipStream_t s = (hipStream_t)stream;
   if (C->dtype == ADMM_DTYPE_F32) {
     BackArgs<float> a{};
@@ -970,6 +966,7 @@ int admm_column_norms_sq(admm_ctx* C, double* W, void* stream) {
 
 int admm_tv_grad(admm_ctx* C, const double* x, double* gx, double* gy, int nimg, void* stream) {
   if (!C || !x || !gx || !gy || nimg < 1) return fail(ADMM_E_INVALID, "bad argument");
+  DEVICE_SCOPE(C->device);
   const int N = C->g.N;
   hipLaunchKernelGGL(k_tv_grad, dim3((N + 63) / 64, (N + 3) / 4, nimg), dim3(kBlock), 0, (hipStream_t)stream, x,
                      gx, gy, N);
@@ -979,6 +976,7 @@ int admm_tv_grad(admm_ctx* C, const double* x, double* gx, double* gy, int nimg,
 
 int admm_tv_div(admm_ctx* C, const double* px, const double* py, double* out, int nimg, void* stream) {
   if (!C || !px || !py || !out || nimg < 1) return fail(ADMM_E_INVALID, "bad argument");
+  DEVICE_SCOPE(C->device);
   const int N = C->g.N;
   hipLaunchKernelGGL(k_tv_div, dim3((N + 63) / 64, (N + 3) / 4, nimg), dim3(kBlock), 0, (hipStream_t)stream, px,
                      py, out, N);
@@ -1007,7 +1005,7 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   const size_t npix = C->npix, m = C->mrays;
   if ((size_t)B.V * npix * 8 >= (1ull << 31) || (size_t)B.V * m * 8 >= (1ull << 31))
     return fail(ADMM_E_INVALID, "batch too large for 32-bit buffer offsets");
-  HIPCHK(hipSetDevice(C->device));
+  DEVICE_SCOPE(C->device);
   HIPCHK(hipDeviceSynchronize());
   RET(free_graphs(C));
   C->b = B;
@@ -1025,11 +1023,9 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   RET(ensure(C->pT, Vp * npix * ds));
   RET(ensure(C->Hp, Vp * npix * ds));
   RET(ensure(C->dsumS, Vp * npix * ds));
-  if (ADMM_TV_FUSE) {
-    RET(ensure(C->x2, (size_t)V * npix * 8));
-    RET(ensure(C->p2, Vp * npix * ds));
-  }
-  if (ADMM_TV_FUSE == 2 && B.cg_iters > 1 && B.cg_iters <= kMaxCgRing)
+  RET(ensure(C->x2, (size_t)V * npix * 8));
+  RET(ensure(C->p2, Vp * npix * ds));
+  if (B.cg_iters > 1 && B.cg_iters <= kMaxCgRing)
     RET(ensure(C->pring, (size_t)(B.cg_iters - 1) * Vp * npix * ds));
   if (B.flags & ADMM_BATCH_KEEP_X) RET(ensure(C->ats, Vp * npix * ds));
   C->ats_valid = false;
@@ -1054,22 +1050,21 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   RET(ensure(C->partE, (size_t)3 * std::max(1, B.n_edges) * C->P_edge * 8));
   RET(ensure(C->redH, (size_t)5 * V * 8 * std::max(1, std::min(B.cg_iters, kMaxCgRing))));
   C->bound = true;
-  if (C->use_graph) {
-    auto fu = [&](hipStream_t s) {
-      return C->dtype == ADMM_DTYPE_F32 ? enqueue_update_any<float>(C, s) : enqueue_update_any<double>(C, s);
+  // the x-update and consensus sequences, recorded once and replayed every iteration
+  auto fu = [&](hipStream_t s) {
+    return C->dtype == ADMM_DTYPE_F32 ? enqueue_update_any<float>(C, s) : enqueue_update_any<double>(C, s);
+  };
+  RET(capture(C, fu, &C->g_update, &C->x_update));
+  if (B.flags & ADMM_BATCH_KEEP_X) {
+    auto fr = [&](hipStream_t s) {
+      return C->dtype == ADMM_DTYPE_F32 ? enqueue_update_any<float>(C, s, true)
+                                        : enqueue_update_any<double>(C, s, true);
     };
-    RET(capture(C, fu, &C->g_update, &C->x_update));
-    if (B.flags & ADMM_BATCH_KEEP_X) {
-      auto fr = [&](hipStream_t s) {
-        return C->dtype == ADMM_DTYPE_F32 ? enqueue_update_any<float>(C, s, true)
-                                          : enqueue_update_any<double>(C, s, true);
-      };
-      RET(capture(C, fr, &C->g_update_reuse, &C->x_update_reuse));
-    }
-    if (B.n_edges > 0) {
-      auto fc = [&](hipStream_t s) { return enqueue_consensus(C, s); };
-      RET(capture(C, fc, &C->g_cons, &C->x_cons));
-    }
+    RET(capture(C, fr, &C->g_update_reuse, &C->x_update_reuse));
+  }
+  if (B.n_edges > 0) {
+    auto fc = [&](hipStream_t s) { return enqueue_consensus(C, s); };
+    RET(capture(C, fc, &C->g_cons, &C->x_cons));
   }
   HIPCHK(hipDeviceSynchronize());
   return ADMM_OK;
@@ -1096,12 +1091,14 @@ int batch_atb(admm_ctx* C, double* atb_out, hipStream_t s) {
 int admm_batch_atb(admm_ctx* C, double* atb_out, void* stream) {
   if (!C || !C->bound) return fail(ADMM_E_STATE, "no batch bound");
   if (!atb_out) return fail(ADMM_E_INVALID, "null atb_out");
+  DEVICE_SCOPE(C->device);
   hipStream_t s = (hipStream_t)stream;
   return C->dtype == ADMM_DTYPE_F32 ? batch_atb<float>(C, atb_out, s) : batch_atb<double>(C, atb_out, s);
 }
 
 int admm_node_update(admm_ctx* C, void* stream) {
   if (!C || !C->bound) return fail(ADMM_E_STATE, "no batch bound");
+  DEVICE_SCOPE(C->device);
   hipStream_t s = (hipStream_t)stream;
   const bool keep = (C->b.flags & ADMM_BATCH_KEEP_X) != 0;
   const bool reuse = keep && C->ats_valid;
@@ -1120,6 +1117,7 @@ int admm_node_update_rounds(admm_ctx* C, int tv_iters, void* stream) {
   if (!C || !C->bound) return fail(ADMM_E_STATE, "no batch bound");
   if (tv_iters < 1) return fail(ADMM_E_INVALID, "tv_iters must be >= 1");
   if (tv_iters == C->b.tv_iters) return admm_node_update(C, stream);
+  DEVICE_SCOPE(C->device);
   hipStream_t s = (hipStream_t)stream;
   const bool keep = (C->b.flags & ADMM_BATCH_KEEP_X) != 0;
   const bool reuse = keep && C->ats_valid;
@@ -1132,6 +1130,7 @@ int admm_node_update_rounds(admm_ctx* C, int tv_iters, void* stream) {
 
 int admm_consensus(admm_ctx* C, void* stream) {
   if (!C || !C->bound) return fail(ADMM_E_STATE, "no batch bound");
+  DEVICE_SCOPE(C->device);
   hipStream_t s = (hipStream_t)stream;
   if (C->x_cons) {
     HIPCHK(hipGraphLaunch(C->x_cons, s));
@@ -1169,6 +1168,7 @@ int time_fwd(admm_ctx* C, int reps, hipStream_t s, float* ms) {
 int admm_time_forward(admm_ctx* C, int reps, void* stream, double* ms_out) {
   if (!C || !C->bound) return fail(ADMM_E_STATE, "no batch bound");
   if (reps < 1 || !ms_out) return fail(ADMM_E_INVALID, "bad argument");
+  DEVICE_SCOPE(C->device);
   hipStream_t s = (hipStream_t)stream;
   float ms = 0.f;
   RET(C->dtype == ADMM_DTYPE_F32 ? time_fwd<float>(C, reps, s, &ms) : time_fwd<double>(C, reps, s, &ms));

@@ -121,9 +121,6 @@ __device__ __forceinline__ void gstore(T* __restrict__ p, const T (&o)[VB]) {
 // deterministic block reduction of NQ float64 values per thread (256 threads);
 // result valid in thread 0.  Fixed shuffle tree + fixed LDS order.
 // ---------------------------------------------------------------------------
-#ifndef ADMM_RS_DPP
-#define ADMM_RS_DPP 1  // wave reductions by gfx950 permlane swaps + DPP (0: __shfl_xor / ds_bpermute)
-#endif
 // float64 lane exchange by DPP (two 32-bit moves); CTRL must describe an exact xor pairing
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double x) {
@@ -172,14 +169,7 @@ template <int NQ>
 __device__ __forceinline__ void block_reduce(double (&v)[NQ], double* lds /* >= 4*NQ */) {
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    double s = v[q];
-    if constexpr (ADMM_RS_DPP) {
-      s = wave_sum_d(s);
-    } else {
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-    }
-    v[q] = s;
+    v[q] = wave_sum_d(v[q]);
   }
   const int wid = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
@@ -198,8 +188,10 @@ __device__ __forceinline__ void block_reduce(double (&v)[NQ], double* lds /* >= 
 // deterministic block reduction of NV (multiple of 16) float64 values per thread
 // by a wave-level reduce-scatter butterfly: at offsets 32, 16, 8, 4 every lane
 // keeps half of its values and adds its partner's copy of that half (NV/2 + NV/4
-// + NV/8 + NV/16 shuffles instead of 6*NV), then a plain butterfly over offsets
-// 2, 1 on the last NV/16.  Lanes with (lane & 3) == 0 then hold the wave totals;
+// + NV/8 + NV/16 exchanges instead of 6*NV), then a plain butterfly over offsets
+// 2, 1 on the last NV/16.  Exchanges are gfx950 permlane32/16 swaps (offsets 32, 16)
+// and DPP row moves (8, 4, 2, 1): every level an exact xor pairing, so the totals are
+// the __shfl_xor butterfly's bit for bit (profiles/r2_reduce_dpp_bitwise.txt).  Lanes with (lane & 3) == 0 then hold the wave totals;
 // the NW waves are combined in LDS in a fixed pairwise tree.  On return thread t < NV of the
 // block can read total t from out_lds[t].  Fixed order -> bitwise reproducible.
 // ---------------------------------------------------------------------------
@@ -210,79 +202,40 @@ __device__ __forceinline__ void block_reduce_rs(double (&v)[NV], double* lds /* 
   static_assert(NV % 16 == 0, "NV must be a multiple of 16");
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  if constexpr (ADMM_RS_DPP) {
-    // the same pairings and additions as the shuffle form below (each level an exact xor
-    // partner; a + b == b + a), so bitwise the same totals, with no LDS traffic and no selects
-    // at offsets 32 and 16: after the swap, lane i of x + y is (keep + partner's send)
-#pragma unroll
-    for (int k = 0; k < NV / 2; ++k) {
-      double x = v[k], y = v[NV / 2 + k];
-      permswap_d<true>(x, y);
-      v[k] = x + y;
-    }
-#pragma unroll
-    for (int k = 0; k < NV / 4; ++k) {
-      double x = v[k], y = v[NV / 4 + k];
-      permswap_d<false>(x, y);
-      v[k] = x + y;
-    }
-    const bool h8 = lane & 8, h4 = lane & 4;
-#pragma unroll
-    for (int k = 0; k < NV / 8; ++k) {  // xor 8 = row_ror:8 within a 16-lane row
-      const double send = h8 ? v[k] : v[NV / 8 + k];
-      const double keep = h8 ? v[NV / 8 + k] : v[k];
-      v[k] = keep + dpp_d<0x128>(send);
-    }
-#pragma unroll
-    for (int k = 0; k < NV / 16; ++k) {  // xor 4: row_shl:4 for lanes with bit 2 clear, row_shr:4 else
-      const double send = h4 ? v[k] : v[NV / 16 + k];
-      const double keep = h4 ? v[NV / 16 + k] : v[k];
-      const double up = dpp_d<0x104>(send), dn = dpp_d<0x114>(send);
-      v[k] = keep + (h4 ? dn : up);
-    }
-#pragma unroll
-    for (int k = 0; k < NV / 16; ++k) {  // xor 2, xor 1: quad_perm [2,3,0,1], [1,0,3,2]
-      double s = v[k];
-      s += dpp_d<0x4E>(s);
-      s += dpp_d<0xB1>(s);
-      v[k] = s;
-    }
-  } else {
+  // at offsets 32 and 16: after the swap, lane i of x + y is (keep + partner's send), with no
+  // LDS traffic and no selects
 #pragma unroll
   for (int k = 0; k < NV / 2; ++k) {
-    const bool hi = lane & 32;
-    const double send = hi ? v[k] : v[NV / 2 + k];
-    const double keep = hi ? v[NV / 2 + k] : v[k];
-    v[k] = keep + __shfl_xor(send, 32, 64);
+    double x = v[k], y = v[NV / 2 + k];
+    permswap_d<true>(x, y);
+    v[k] = x + y;
   }
 #pragma unroll
   for (int k = 0; k < NV / 4; ++k) {
-    const bool hi = lane & 16;
-    const double send = hi ? v[k] : v[NV / 4 + k];
-    const double keep = hi ? v[NV / 4 + k] : v[k];
-    v[k] = keep + __shfl_xor(send, 16, 64);
+    double x = v[k], y = v[NV / 4 + k];
+    permswap_d<false>(x, y);
+    v[k] = x + y;
+  }
+  const bool h8 = lane & 8, h4 = lane & 4;
+#pragma unroll
+  for (int k = 0; k < NV / 8; ++k) {  // xor 8 = row_ror:8 within a 16-lane row
+    const double send = h8 ? v[k] : v[NV / 8 + k];
+    const double keep = h8 ? v[NV / 8 + k] : v[k];
+    v[k] = keep + dpp_d<0x128>(send);
   }
 #pragma unroll
-  for (int k = 0; k < NV / 8; ++k) {
-    const bool hi = lane & 8;
-    const double send = hi ? v[k] : v[NV / 8 + k];
-    const double keep = hi ? v[NV / 8 + k] : v[k];
-    v[k] = keep + __shfl_xor(send, 8, 64);
+  for (int k = 0; k < NV / 16; ++k) {  // xor 4: row_shl:4 for lanes with bit 2 clear, row_shr:4 else
+    const double send = h4 ? v[k] : v[NV / 16 + k];
+    const double keep = h4 ? v[NV / 16 + k] : v[k];
+    const double up = dpp_d<0x104>(send), dn = dpp_d<0x114>(send);
+    v[k] = keep + (h4 ? dn : up);
   }
 #pragma unroll
-  for (int k = 0; k < NV / 16; ++k) {
-    const bool hi = lane & 4;
-    const double send = hi ? v[k] : v[NV / 16 + k];
-    const double keep = hi ? v[NV / 16 + k] : v[k];
-    v[k] = keep + __shfl_xor(send, 4, 64);
-  }
-#pragma unroll
-  for (int k = 0; k < NV / 16; ++k) {
+  for (int k = 0; k < NV / 16; ++k) {  // xor 2, xor 1: quad_perm [2,3,0,1], [1,0,3,2]
     double s = v[k];
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 1, 64);
+    s += dpp_d<0x4E>(s);
+    s += dpp_d<0xB1>(s);
     v[k] = s;
-  }
   }
   if ((lane & 3) == 0) {
     const int base = ((lane >> 5) & 1) * (NV / 2) + ((lane >> 4) & 1) * (NV / 4) + ((lane >> 3) & 1) * (NV / 8) +
@@ -532,32 +485,8 @@ constexpr int kFgG = ADMM_FG_G;        // max angles (waves) per block
 constexpr int kFgThreads = 64 * kFgG;
 constexpr int kFgWin = ADMM_FG_WIN;    // staged window width (pixels)
 constexpr int kFgSeg = ADMM_FG_SEG;    // row segments (partial sums) per ray
-#ifndef ADMM_FG_PRIO
-#define ADMM_FG_PRIO 1  // wave priority raised while issuing the staging loads (2: during taps; 0: off)
-#endif
-#ifndef ADMM_FG_W4
-#define ADMM_FG_W4 1  // chunk window origins as one int4 LDS read into scalars (0: one read per row)
-#endif
-#ifndef ADMM_FG_DMA
-#define ADMM_FG_DMA 1  // LDS-DMA staging of 16-byte sample planes (0: register staging)
-#endif
-#ifndef ADMM_FG_PIPE
-#define ADMM_FG_PIPE 1  // software-pipelined taps of full chunks in the LDS-DMA kernel (0: row by row)
-#endif
 #ifndef ADMM_FG_DMA_ROWS
 #define ADMM_FG_DMA_ROWS 2  // rows per chunk of the LDS-DMA kernel (4: 34.7 us, 1: 38.0 us at 512^2 vs 32.5)
-#endif
-#ifndef ADMM_FG_WPAR
-#define ADMM_FG_WPAR 1  // row windows from all G waves with LDS min/max atomics (0: serial loop over angles)
-#endif
-#ifndef ADMM_FG_DMAMASK
-#define ADMM_FG_DMAMASK 0  // 1: LDS-DMA lanes past a row's touched width fetch nothing (+0.7 us: the select costs more than the fetch)
-#endif
-#ifndef ADMM_FG_IDLE_SKIP
-#define ADMM_FG_IDLE_SKIP 1  // waves beyond the group's angle count skip the tap loop (0: tuning A/B)
-#endif
-#ifndef ADMM_FG_EO
-#define ADMM_FG_EO 1  // even/odd half-window LDS layout (0: plain pixel order, tuning only)
 #endif
 constexpr int kFgHalf = kFgWin / 2;        // slots per parity
 constexpr int kFgOdd = kFgHalf + 4;        // odd half-window offset (+64 B bank shift)
@@ -622,7 +551,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   // hardware, scripts/probes/dma_oob.hip), two chunk buffers, one barrier per chunk, and no
   // VGPRs or ds_write instructions spent on staging.  float64 x 8 nodes (4 planes) keeps the
   // register-staged single buffer (two would not fit two blocks per CU).
-  constexpr bool kDma = ADMM_FG_DMA && sizeof(Pack<T, PV>) == 16 && NPL <= 2;
+  constexpr bool kDma = sizeof(Pack<T, PV>) == 16 && NPL <= 2;
   // rows per staged chunk (2 in the LDS-DMA kernel: the next chunk's DMA is issued a
   // 2-row chunk of taps ahead; 4-row chunks, or a 3/4-buffer ring with counted vmcnt waits
   // keeping 2-3 chunks in flight, measured slower)
@@ -632,58 +561,37 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   // every row window of the segment (N <= 4096): origin and the width actually touched
   __shared__ __align__(16) int wlo_s[(4096 + kFgSeg - 1) / kFgSeg + 4];  // +4: int4 reads of the last chunk
   __shared__ int wnum_s[(4096 + kFgSeg - 1) / kFgSeg + 4];
-  if constexpr (ADMM_FG_WPAR) {
-    // Row windows in parallel: wave g < G bounds its own angle's rays on every row and
-    // folds floor(l) into the row's min / max with LDS integer atomics (floor is monotone,
-    // so min/max of floors == floor of min/max: the same windows as the serial loop below,
-    // in any order).  The serial form walks the G angles one dependent global load at a
-    // time on 64 threads, exposed at the start of every block.
-    for (int r = threadIdx.x; r < nrows; r += kFgThreads) {
-      wlo_s[r] = INT_MAX;
-      wnum_s[r] = INT_MIN;  // floor(lmax) until the fix-up below
-    }
-    __syncthreads();
-    if (g < G) {  // wave-uniform; a == ang[t0 + g] here
-      const int ka = max(kbase + gr->delta[seg][g], 0), kb = min(kbase + gr->delta[seg][g] + 63, n_det - 1);
-      if (ka <= kb) {
-        const double ca = fma((double)ka, a.A1, a.A0), cb = fma((double)kb, a.A1, a.A0);
-        for (int r = lane; r < nrows; r += 64) {
-          const double dm = (double)(m_lo + r);
-          const double la = fma(dm, a.dl, ca), lb = fma(dm, a.dl, cb);
-          atomicMin(&wlo_s[r], (int)floor(fmin(la, lb)));
-          atomicMax(&wnum_s[r], (int)floor(fmax(la, lb)));
-        }
+  // Row windows in parallel: wave g < G bounds its own angle's rays on every row and
+  // folds floor(l) into the row's min / max with LDS integer atomics (floor is monotone,
+  // so min/max of floors == floor of min/max: the windows do not depend on the order).
+  // The window origin is even: a tap's even/odd LDS half, and so the order of a ray's two
+  // FMAs per row, then follows the absolute pixel parity -- identical for every group / ray
+  // layout / block order, so results do not depend on the plan (or on the GPU count that
+  // chooses it).  The one extra column fits the host's 2-pixel window margin.
+  for (int r = threadIdx.x; r < nrows; r += kFgThreads) {
+    wlo_s[r] = INT_MAX;
+    wnum_s[r] = INT_MIN;  // floor(lmax) until the fix-up below
+  }
+  __syncthreads();
+  if (g < G) {  // wave-uniform; a == ang[t0 + g] here
+    const int ka = max(kbase + gr->delta[seg][g], 0), kb = min(kbase + gr->delta[seg][g] + 63, n_det - 1);
+    if (ka <= kb) {
+      const double ca = fma((double)ka, a.A1, a.A0), cb = fma((double)kb, a.A1, a.A0);
+      for (int r = lane; r < nrows; r += 64) {
+        const double dm = (double)(m_lo + r);
+        const double la = fma(dm, a.dl, ca), lb = fma(dm, a.dl, cb);
+        atomicMin(&wlo_s[r], (int)floor(fmin(la, lb)));
+        atomicMax(&wnum_s[r], (int)floor(fmax(la, lb)));
       }
     }
-    __syncthreads();
-    for (int r = threadIdx.x; r < nrows; r += kFgThreads) {
-      const int fmn = wlo_s[r], fmx = wnum_s[r];
-      const bool any = fmn != INT_MAX;  // always true for host-planned chunks
-      const int wlo = (fmn - 1) & ~1;   // even origin, as below
-      wlo_s[r] = any ? wlo : 0;
-      wnum_s[r] = any ? min(kFgWin, fmx - wlo + 2) : 0;
-    }
-  } else
+  }
+  __syncthreads();
   for (int r = threadIdx.x; r < nrows; r += kFgThreads) {
-    const double dm = (double)(m_lo + r);
-    double lmin = 1e300, lmax = -1e300;
-    for (int gg = 0; gg < G; ++gg) {
-      const FwdAngle b = ang[t0 + gg];
-      const int ka = max(kbase + gr->delta[seg][gg], 0), kb = min(kbase + gr->delta[seg][gg] + 63, n_det - 1);
-      if (ka > kb) continue;  // no ray of this angle in the block
-      const double la = fma(dm, b.dl, fma((double)ka, b.A1, b.A0));
-      const double lb = fma(dm, b.dl, fma((double)kb, b.A1, b.A0));
-      lmin = fmin(lmin, fmin(la, lb));
-      lmax = fmax(lmax, fmax(la, lb));
-    }
-    const bool any = lmin <= lmax;  // always true for host-planned chunks
-    // even window origin: a tap's even/odd LDS half, and so the order of a ray's two FMAs
-    // per row, then follows the absolute pixel parity -- identical for every group / ray
-    // layout / block order, so results do not depend on the plan (or on the GPU count that
-    // chooses it).  The one extra column fits the host's 2-pixel window margin.
-    const int wlo = ((int)floor(lmin) - 1) & ~1;
+    const int fmn = wlo_s[r], fmx = wnum_s[r];
+    const bool any = fmn != INT_MAX;  // always true for host-planned chunks
+    const int wlo = (fmn - 1) & ~1;   // even origin, as below
     wlo_s[r] = any ? wlo : 0;
-    wnum_s[r] = any ? min(kFgWin, (int)floor(lmax) - wlo + 2) : 0;
+    wnum_s[r] = any ? min(kFgWin, fmx - wlo + 2) : 0;
   }
   __syncthreads();
 
@@ -694,18 +602,15 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   T acc[VB];
 #pragma unroll
   for (int u = 0; u < VB; ++u) acc[u] = T(0);
-#ifndef ADMM_FG_EXPT
-#define ADMM_FG_EXPT 0  // timing diagnostics only: 1 = no tap loop, 2 = no staging
-#endif
   int wl_cur[R];  // the current chunk's window origins (scalars)
   // the chunk's window origins, read once into scalar registers (a per-row LDS read
   // would put a dependent LDS round trip in front of every row's tap reads)
   auto origins = [&](int m0, int (&wl)[R]) {
-    if constexpr (ADMM_FG_W4 && R == 2) {  // one LDS round trip for both rows
+    if constexpr (R == 2) {  // one LDS round trip for both rows
       const int2 w2 = *reinterpret_cast<const int2*>(&wlo_s[m0 - m_lo]);
       wl[0] = w2.x;
       wl[1] = w2.y;
-    } else if constexpr (ADMM_FG_W4 && R == 4) {
+    } else if constexpr (R == 4) {
       const int4 w4 = *reinterpret_cast<const int4*>(&wlo_s[m0 - m_lo]);
       wl[0] = __builtin_amdgcn_readfirstlane(w4.x);
       wl[1] = __builtin_amdgcn_readfirstlane(w4.y);
@@ -735,20 +640,9 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       }
       const T w0 = T(1) - w1;
       // taps idx (weight w0) and idx+1 (w1): one is even, one odd
-      int se, so;
-      T we, wo;
-      if constexpr (ADMM_FG_EO) {
-        const bool odd = idx & 1;
-        se = (idx + 1) >> 1;
-        so = kFgOdd + (idx >> 1);
-        we = odd ? w1 : w0;
-        wo = odd ? w0 : w1;
-      } else {  // plain layout (tuning comparison): left tap, then right tap
-        se = idx;
-        so = idx + 1;
-        we = w0;
-        wo = w1;
-      }
+      const bool odd = idx & 1;
+      const int se = (idx + 1) >> 1, so = kFgOdd + (idx >> 1);
+      const T we = odd ? w1 : w0, wo = odd ? w0 : w1;
 #pragma unroll
       for (int q = 0; q < NPL; ++q) {
         const Pack<T, PV> s0 = wb[q][r][se];
@@ -761,7 +655,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       }
     }
   };
-  // Software-pipelined full chunk (ADMM_FG_PIPE): every row's tap slots and weights first,
+  // Software-pipelined full chunk: every row's tap slots and weights first,
   // then row r+1's LDS reads issued before row r's FMAs, so one row's reads are always in
   // flight behind the other's arithmetic (the LDS-DMA staging freed the registers: the
   // register-staged kernel had no room for the second row's 16).  Same FMAs, same order.
@@ -829,7 +723,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   };
   // waves g >= G (groups smaller than kFgG) only stage and meet the barriers: their taps
   // would repeat angle G-1's and burn the LDS bandwidth the real taps are bound by
-  const bool idle = ADMM_FG_EXPT == 1 || (ADMM_FG_IDLE_SKIP && g >= G);
+  const bool idle = g >= G;
 
   if constexpr (kDma) {
     // one 1-KiB piece per wave-instruction: 64 consecutive 16-B slots of one (plane, row,
@@ -851,17 +745,17 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(rb >> 32));
         const __amdgpu_buffer_rsrc_t rs =
             make_rsrc((const void*)(uintptr_t)(((uint64_t)hi << 32) | lo), rowbytes);
-        const int rel = 128 * h + par + 2 * lane, col = wo + rel;
-        // negative columns wrap to huge unsigned offsets: out of range, zero-filled; so are
-        // slots past the row's touched width (never read by a tap: no L2 fetch spent on them)
-        const unsigned voff = (!ADMM_FG_DMAMASK || rel < wn) ? (unsigned)((col * VB + pl * PV) * (int)sizeof(T))
-                                                             : 0x7ffffff0u;
+        const int col = wo + 128 * h + par + 2 * lane;
+        // negative columns wrap to huge unsigned offsets: out of range, zero-filled (slots past
+        // the row's touched width are fetched but never read by a tap: masking them cost more
+        // VALU than the L2 fetch it saved)
+        const unsigned voff = (unsigned)((col * VB + pl * PV) * (int)sizeof(T));
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             rs, (__attribute__((address_space(3))) void*)&win[b][pl][r][(par ? kFgOdd : 0) + 64 * h], 16, voff,
             0, 0, 0);
       }
     };
-    if (ADMM_FG_EXPT != 2) dma(m_lo, 0);
+    dma(m_lo, 0);
     __syncthreads();  // (its fence waits for this wave's LDS-DMA: vmcnt(0)) chunk 0 staged
     // one chunk: DMA of the next one into the other buffer, then this one's taps.  The
     // buffer index is a compile-time constant (the loop is unrolled by the two buffers), so
@@ -870,10 +764,10 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
     auto step = [&](auto cbc, int m0) __attribute__((always_inline)) {
       constexpr int cb = decltype(cbc)::value;
       // the other buffer was last read by the previous chunk's taps (done: barrier below)
-      if (ADMM_FG_EXPT != 2 && m0 + R < m_hi) dma(m0 + R, cb ^ 1);
+      if (m0 + R < m_hi) dma(m0 + R, cb ^ 1);
       origins(m0, wl_cur);
       const int rows = idle ? 0 : min(R, m_hi - m0);
-      if (ADMM_FG_PIPE && ADMM_FG_EO && rows == R)
+      if (rows == R)
         taps4(win[cb], m0);
       else
         taps(win[cb], m0, rows, wl_cur);
@@ -913,23 +807,22 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         if (q < R * kFgWin * NPL) {
           const int pl = q % NPL, rw = q / NPL;
           const int r = rw / kFgWin, w = rw - r * kFgWin;
-          win[0][pl][r][ADMM_FG_EO ? ((w & 1) ? kFgOdd + (w >> 1) : (w >> 1)) : w] = stage[e];
+          win[0][pl][r][(w & 1) ? kFgOdd + (w >> 1) : (w >> 1)] = stage[e];
         }
       }
     };
-    if (ADMM_FG_EXPT != 2) fetch(m_lo);
+    fetch(m_lo);
     for (int m0 = m_lo; m0 < m_hi; m0 += R) {
       int wl[R];
       origins(m0, wl);
       __syncthreads();  // previous chunk's readers are done
-      if (ADMM_FG_EXPT != 2) commit();
+      commit();
       __syncthreads();
-      if (ADMM_FG_PRIO == 1) __builtin_amdgcn_s_setprio(1);
-      if (ADMM_FG_EXPT != 2 && m0 + R < m_hi) fetch(m0 + R);
-      if (ADMM_FG_PRIO == 1) __builtin_amdgcn_s_setprio(0);
-      if (ADMM_FG_PRIO == 2) __builtin_amdgcn_s_setprio(1);
+      // the next chunk's loads issue at raised wave priority (ahead of other waves' taps)
+      __builtin_amdgcn_s_setprio(1);
+      if (m0 + R < m_hi) fetch(m0 + R);
+      __builtin_amdgcn_s_setprio(0);
       taps(win[0], m0, idle ? 0 : min(R, m_hi - m0), wl);
-      if (ADMM_FG_PRIO == 2) __builtin_amdgcn_s_setprio(0);
     }
   }
   if (g < G && k >= 0 && k < n_det) {
@@ -1206,12 +1099,6 @@ constexpr int kBWin = ((ce_isqrt_ceil((kBTJ - 1) * (kBTJ - 1) + (kBTI - 1) * (kB
 #endif
 constexpr int kBAngC = ADMM_BK_ANGC;  // angles per staged sinogram-window chunk
 
-#ifndef ADMM_BK_PF
-#define ADMM_BK_PF 1  // register-prefetched sinogram windows (0: stage each chunk after its kmin)
-#endif
-#ifndef ADMM_BK_EXPT
-#define ADMM_BK_EXPT 0  // timing diagnostics only: 1 = no angle loop, 2 = no window loads, 3 = no H epilogue
-#endif
 // DIAG epilogue for a whole kBTJ x kBTI tile (block-cooperative; replaces the per-pixel
 // DIAG branch of back_epilogue, same formulas in the same order, so bitwise the same):
 // per node, x over the tile plus one halo row/column on each side is staged in LDS and
@@ -1388,12 +1275,12 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
     }
   };
 
-  // sinogram windows (MODE != WSQ).  ADMM_BK_PF: the next chunk's window is fetched into
+  // sinogram windows (MODE != WSQ).  PF: the next chunk's window is fetched into
   // registers before this chunk's taps and written to LDS after them (the single block per
   // CU otherwise waits for every chunk's loads with nothing to overlap; +12 VGPRs, still
   // 4 waves/SIMD); kmin is double-buffered.  Otherwise: compute kmin, stage, tap per chunk.
   // (float samples, H/INIT modes: the float64 and DIAG variants would spill)
-  constexpr bool PF = ADMM_BK_PF && std::is_same<T, float>::value && (MODE == BACK_H || MODE == BACK_INIT ||
+  constexpr bool PF = std::is_same<T, float>::value && (MODE == BACK_H || MODE == BACK_INIT ||
                                                                      MODE == BACK_PLAIN || MODE == BACK_ATB);
   constexpr int SPER = (ANGC * kBWin * NPL + kBkThreads - 1) / kBkThreads;
   Pack<T, PV> wst[SPER];
@@ -1414,7 +1301,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
       const int pl = q % NPL, aw = q / NPL;
       const int a = aw / kBWin, w = aw - a * kBWin;
       const int k = (a < nt) ? a * kBWin - reinterpret_cast<const int*>(kmin_s[buf])[a] / PB + w - kbias : -1;
-      if (ADMM_BK_EXPT != 2 && a < nt && k >= 0 && k < n_det) {
+      if (a < nt && k >= 0 && k < n_det) {
         wst[e] = *reinterpret_cast<const Pack<T, PV>*>(sino_c + ((size_t)(t0 + a) * n_det + k) * VB + pl * PV);
       } else {
 #pragma unroll
@@ -1474,7 +1361,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
     // lgkmcnt(0) per group -- scalar and LDS loads share that counter), then its taps
     // run on LDS reads alone
     t0c = t0;
-    int tt = (ADMM_BK_EXPT == 1) ? nt : 0;
+    int tt = 0;
     for (; tt + 4 <= nt; tt += 4) {
       BackAngleC g[4];
 #pragma unroll
@@ -1527,11 +1414,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
     __shared__ double diag_s[(kBTI + 2) * (kBTJ + 2) + 2 * (kBTI + 1) * (kBTJ + 1)];
     diag_epilogue_tile<T, VB>(A, diag_s, ib, jb, i, j, inb, chunk, v0, nv, acc, pq);
   } else if (inb) {
-    if constexpr (ADMM_BK_EXPT == 3 && MODE == BACK_H) {
-      gstore<T, VB>(A.out_t + (size_t)chunk * N * N * VB + (size_t)(i * N + j) * VB, acc);
-    } else {
-      back_epilogue<T, VB, MODE, NQ>(A, i, j, chunk, v0, nv, acc, pq);
-    }
+    back_epilogue<T, VB, MODE, NQ>(A, i, j, chunk, v0, nv, acc, pq);
   }
 
   if constexpr (MODE == BACK_H || MODE == BACK_DIAG) {
@@ -1720,15 +1603,12 @@ __global__ __launch_bounds__(kBlock) void k_transpose(const T* __restrict__ in, 
 // runs (a node-per-lane mapping splits those into 64-B pieces across 8 arrays 2 MB apart).
 constexpr int kCgRows = kBlock / kTile;  // 8 rows x 32 columns per block
 
-#ifndef ADMM_TV_FUSE
-#define ADMM_TV_FUSE 2  // CG x steps applied by the TV update: 2 all K (direction ring), 1 the round's last one, 0 none
-#endif
-#ifndef ADMM_CG_SKIP_P
-#define ADMM_CG_SKIP_P 1  // 0: every CG step writes p (A/B timing only)
-#endif
+// The CG x steps of a split-Bregman round are applied by the TV update that ends the round
+// (k_tv_update FUSE): all K of them from a ring of the round's directions when K <=
+// kMaxCgRing, else only the round's last one.
 // WRITE_P = false: the last CG step of a split-Bregman round -- the TV update (or the next
 // x-update's start) overwrites p and its transposed copy, so only x and r are written
-// WRITE_X = false (ADMM_TV_FUSE 2): x is left alone -- the TV update applies the round's
+// WRITE_X = false (direction ring): x is left alone -- the TV update applies the round's
 // x += alpha_k p_k, k = 0..K-1, in the same order (so bitwise the same x) from the p ring;
 // p_{k+1} then goes to its own slot pout (p_k stays readable for that).
 template <typename T, int VB, bool WRITE_P = true, bool WRITE_X = true>
@@ -1817,8 +1697,8 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
-// FUSE: the round's CG x steps are folded in (ADMM_TV_FUSE 2: all K of them, the CG updates
-// leaving x alone and keeping each direction p_k in a ring slot; 1: only the last one).
+// FUSE: the round's CG x steps are folded in (all K of them, the CG updates leaving x alone
+// and keeping each direction p_k in a ring slot; K > kMaxCgRing: only the last one).
 // x after those steps is formed once per pixel of the stencil region, from the old x and
 // p_k with the same fmas in the same order, written once to xout (x ping-pongs: neighbour
 // blocks still read the old x), and r gets the last step's update and the TV shift in one
@@ -1826,16 +1706,13 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // as the separate kernels (scripts/check_bitwise.py).
 // The CG directions whose x steps the fused TV update applies (FUSE): p[k] with alpha_k
 // from the reduction redH + k * 5V, k = 0 .. K-1 (K = 1: only the round's last step).
-#ifndef ADMM_TV_USTATE
-#define ADMM_TV_USTATE 1  // between an x-update's TV rounds keep u = Kx + e only (see k_tv_update)
-#endif
 constexpr int kMaxCgRing = 8;
 template <typename T>
 struct PRing {
   const T* p[kMaxCgRing];
   int K;
 };
-// UIN / UOUT (ADMM_TV_USTATE): between the rounds of one x-update the split-Bregman state
+// UIN / UOUT: between the rounds of one x-update the split-Bregman state
 // is kept as u = Kx + e_old alone (2 doubles per pixel instead of d and e, 4): the next
 // round recomputes d = shrink(u) and e = u - d -- exactly the values the round that wrote
 // u computed, so the iteration is bitwise the same -- and the traffic of a middle round

@@ -7,7 +7,7 @@ sys.path.insert(0, "distributed-inverse-problem-admm_amd")
 from admm_hip.build import build  # noqa: E402
 
 os.makedirs("variants", exist_ok=True)
-# each argument: NAME:MACRO=VAL,MACRO=VAL   e.g.  ldsrec0:ADMM_BACK_LDSREC=0
+# each argument: NAME:MACRO=VAL,MACRO=VAL   e.g.  seg16:ADMM_FG_SEG=16
 variants = []
 for a in sys.argv[1:]:
     name, _, defs = a.partition(":")

@@ -1,0 +1,52 @@
+"""CPU: bench.py's launch decision (driver contract).
+
+* ``--gpus N`` under a launcher must equal WORLD_SIZE (an error, not a warning);
+* without a launcher and N > 1, bench.py starts the N ranks itself and fails when a rank
+  fails (here every rank fails: no GPU in this container), without hanging.
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(kw)
+    return env
+
+
+def test_gpus_must_match_world_size():
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=120, env=_env(WORLD_SIZE="3", RANK="0", LOCAL_RANK="0"))
+    assert p.returncode == 2 and "must match" in p.stderr
+    assert p.stdout.strip() == ""
+
+
+def test_self_launch_propagates_rank_failure():
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1",
+                        "--strong", "none"], cwd=ROOT, capture_output=True, text=True, timeout=300,
+                       env=_env(ADMM_DIST_BACKEND="gloo", CUDA_VISIBLE_DEVICES=""))
+    assert p.returncode != 0
+    assert "exited with" in p.stderr
+    assert not any(l.startswith("{") for l in p.stdout.splitlines())
+
+
+def test_cpu_baseline_reports_eq1_certificate():
+    """The bench's CPU leg (oracle x-updates of node 0) carries rel_fro and the eq.(1)
+    certificate of the oracle image; small case (32^2, 45 angles, 2 processes, 1 s)."""
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    import bench
+    from oracle.geometry import Geometry, joseph_matrix, shepp_logan
+    N, a = 32, 45
+    A = joseph_matrix(Geometry(N, a))
+    b = A @ shepp_logan(N, 2).ravel() + 0.005 * np.random.default_rng(0).standard_normal(A.shape[0])
+    q = np.maximum(np.asarray(A.multiply(A).sum(axis=0)).ravel(), 1e-12)
+    r = bench.cpu_baseline(N, a, b, q, np.zeros(N * N), procs=2, budget=1.0)
+    assert r["kind"] == "port" and r["cores"] == 2 and r["value"] > 0
+    assert abs(r["rel_fro"] - 1.0) < 1e-12  # x_gpu = 0 here
+    c = r["eq1_gap"]
+    assert c["m"] > 0 and c["dist_bound"] > 0 and c["obj_gap_bound"] >= c["eps"] >= 0
+    assert c["dist_bound"] >= c["stationarity"] / c["m"]

@@ -132,7 +132,7 @@ def test_ragged_image_and_node_chunks(cuda):
 
 def test_cg_steps_beyond_the_direction_ring(cuda):
     """cg_iters = 9 > the 8-slot direction ring: the TV update then folds in only the round's
-    last CG step (ADMM_TV_FUSE 1 path) -- same iteration, same oracle."""
+    last CG step (the F = 1 path of enqueue_update) -- same iteration, same oracle."""
     compare(nx.cycle_graph(4), 32, 4, 3, 96, tv_iters=2, cg_iters=9)
 
 

@@ -12,9 +12,9 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(*args):
+def _run(*args, env=None):
     out = subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, capture_output=True, text=True,
-                         timeout=300, check=True).stdout
+                         timeout=300, check=True, env=env).stdout
     lines = [l for l in out.splitlines() if l.strip().startswith("{")]
     assert len(lines) == 1, out
     return json.loads(lines[0])
@@ -36,6 +36,16 @@ def test_bench_line_contract(cuda):
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
     assert 0 < r["lds"]["frac"] <= 1
     assert "workload" in b["config"] and "model" not in b["config"]
+
+
+def test_bench_launches_its_own_ranks(cuda):
+    """``python bench.py --gpus 2`` with no launcher spawns the two ranks itself (gloo on
+    this one-GPU box; the driver's nccl default is unchanged) and relays rank 0's line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["ADMM_DIST_BACKEND"] = "gloo"
+    b = _run("--gpus", "2", "--steps", "2", "--warmup", "1", "--strong", "none", env=env)
+    assert b["n_gpus"] == 2 and b["config"]["nodes"] == 16
+    assert b["exchange_check"]["ok"] and b["exchange_check"]["halo_rows"] == 4
 
 
 def test_bench_config_line(cuda):

@@ -91,3 +91,33 @@ def test_grouped_forward_default_angles(cuda):
     """C1-style per-node angle counts (180 total over 4 nodes = 45: one angle at pi/2)."""
     _check(64, 45, "float32", 4, 1, seed=45)
     _check(64, 45, "float64", 4, 0, seed=46)
+
+
+def _check_adjoint(N, a, dtype, k, seed, tol):
+    """A^T y with y nonzero only on the sampled angles, against the Joseph CSR matrix of those
+    angles transposed (k_back's tap loop -- every mode shares it -- at full size)."""
+    op = RayTransform(ParallelBeamGeometry(N, a), dtype)
+    tdt = torch.float64 if dtype == "float64" else torch.float32
+    sel = _angle_subset(a)
+    rng = np.random.default_rng(seed)
+    Y = np.zeros((k, a, N))
+    Y[:, sel, :] = rng.standard_normal((k, len(sel), N))
+    Yt = torch.as_tensor(Y.reshape(k, a * N), dtype=tdt)
+    X = (op.T @ Yt.cuda()).double().cpu().numpy()
+    torch.cuda.synchronize()
+    A = joseph_matrix(Geometry(N, a), angles=sel)
+    Ys = Yt.double().numpy().reshape(k, a, N)[:, sel, :].reshape(k, -1)
+    worst = max(float(np.linalg.norm(X[v] - A.T @ Ys[v]) / np.linalg.norm(A.T @ Ys[v])) for v in range(k))
+    assert worst < tol, (N, a, dtype, worst)
+    return worst
+
+
+def test_adjoint_1024_float32(cuda):
+    """C4 size: A^T at 1024^2, 96 angles, float32 samples (k_back was pinned at
+    <= 128^2 only; the C4 operator-level oracle uses this A^T)."""
+    _check_adjoint(1024, 96, "float32", 2, 11, 4e-6)
+
+
+def test_adjoint_2048_float64(cuda):
+    """C5 size and precision: A^T at 2048^2, 96 angles, float64 samples."""
+    _check_adjoint(2048, 96, "float64", 1, 12, 1e-12)

@@ -4,7 +4,10 @@ gather_images) with 2 ranks sharing one GPU over gloo, against 1 rank.
 The real configuration is one rank per GPU over RCCL; this runs the same
 kernels and plan/exchange code with gloo (host-staged copies) so the N>1 path
 is exercised on the device in a 1-GPU session.  Trajectories and images must
-be bitwise identical to the single-rank run.
+be bitwise identical to the single-rank run.  The "unequal" case
+splits 100 angles over 6 nodes (17,17,17,17,16,16: the reference's own remainder rule,
+block_2_load_odl_data.py:35-38), so nodes with different operators run as separate device
+batches (admm_hip/groups.py) within a rank as well as across ranks.
 """
 import os
 import socket
@@ -28,7 +31,7 @@ def _free_port():
     return p
 
 
-def _problem():
+def _problem(angles=96):
     import sys
     for p in (os.path.join(ROOT, "distributed-inverse-problem-admm_amd"), ROOT):
         if p not in sys.path:
@@ -36,16 +39,16 @@ def _problem():
     from admm_hip.data import make_precisions, make_sinograms, shepp_logan
     from admm_hip.solver import make_operators
     N, V = 40, 6
-    ops = make_operators(N, V, 96, device=0)
+    ops = make_operators(N, V, angles, device=0)
     ph = shepp_logan(N)
     sinos = make_sinograms(ops, ph, 0.005, seed=1000)
     Wi, Q = make_precisions(ops)
     return N, V, ops, ph, sinos, Wi, Q
 
 
-def _run(graph, fusion, group=None):
+def _run(graph, fusion, angles=96, group=None):
     from block_6_admm_loop_ver2 import decentralized_admm
-    N, V, ops, ph, sinos, Wi, Q = _problem()
+    N, V, ops, ph, sinos, Wi, Q = _problem(angles)
     G = {"ring": nx.cycle_graph(V), "complete": nx.complete_graph(V)}[graph]
     if fusion == "weighted":
         rng = np.random.default_rng(2)
@@ -56,7 +59,7 @@ def _run(graph, fusion, group=None):
     return np.stack(x), {k: np.asarray(h[k]) for k in ("primal", "dual", "obj_total", "mse_sino_total")}
 
 
-def _worker(rank, world, port, graph, fusion, q):
+def _worker(rank, world, port, graph, fusion, angles, q):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -64,18 +67,20 @@ def _worker(rank, world, port, graph, fusion, q):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank, _run(graph, fusion)))
+        q.put((rank, _run(graph, fusion, angles)))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("graph,fusion", [("ring", "midpoint"), ("complete", "weighted")])
-def test_two_ranks_on_one_gpu_match_one_rank_bitwise(cuda, graph, fusion):
-    x1, h1 = _run(graph, fusion)
+@pytest.mark.parametrize("graph,fusion,angles", [("ring", "midpoint", 96), ("complete", "weighted", 96),
+                                                ("complete", "midpoint", 100), ("ring", "weighted", 100)],
+                         ids=["ring", "complete-weighted", "unequal-complete", "unequal-ring-weighted"])
+def test_two_ranks_on_one_gpu_match_one_rank_bitwise(cuda, graph, fusion, angles):
+    x1, h1 = _run(graph, fusion, angles)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, graph, fusion, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, graph, fusion, angles, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in procs)

@@ -117,6 +117,34 @@ def problem(gname):
     return G, V, N, A, ph, sinos, W
 
 
+def test_subset_plans_of_operator_groups():
+    """Groups of one rank's nodes (admm_hip/groups.py): every group holds every edge incident
+    to it, each edge is owned by exactly one group (the one with its lower endpoint), halo
+    rows are exactly the out-of-group neighbours, and incidence lists keep G.neighbors order."""
+    from admm_hip.plan import make_plan, make_subset_plan
+    G = nx.erdos_renyi_graph(12, 0.4, seed=3)
+    rp = make_plan(G, 12, 2, 1)  # nodes 6..11
+    groups = [[6, 8, 9], [7, 11], [10]]
+    plans = [make_subset_plan(G, 12, g, 2, 1, rp.ranges, rp.edges) for g in groups]
+    owned = {}
+    for P, g in zip(plans, groups):
+        assert P.local_nodes == sorted(g)
+        nb = {j for i in g for j in G.neighbors(i)} - set(g)
+        assert P.halo_nodes == sorted(nb)
+        for k, ge in enumerate(P.stored_edges):
+            a, b = P.edges[ge]
+            assert a in g or b in g
+            assert P.edge_a_row[k] == P.xrow[a] and P.edge_b_row[k] == P.xrow[b]
+            if P.owned_edge[k]:
+                assert ge not in owned and a in g
+                owned[ge] = True
+        for k, i in enumerate(P.local_nodes):
+            nbrs = [P.inc_nbr[q] for q in range(P.inc_off[k], P.inc_off[k + 1])]
+            assert nbrs == list(G.neighbors(i))
+    # together the groups own exactly the edges the rank plan owns
+    assert sorted(owned) == sorted(ge for k, ge in enumerate(rp.stored_edges) if rp.owned_edge[k])
+
+
 def run_sharded(rank, world, gname, HaloExchange, assemble_stats, gather_images, make_plan):
     """The device loop of admm_hip.admm.run_admm with the oracle in place of the kernels."""
     from oracle import node_solver as ons
