@@ -99,8 +99,6 @@ struct admm_ctx {
   double Kb = 0.0;  // angle-independent part of the back projector's k_f
   int kbias = 0;    // integer bias making every pixel's k_f positive (k_back)
   int wexp = 0;     // k_back float weights scaled by 2^-wexp (<= 1 for the fma clamp)
-  Buf bkwin;        // k_back window origins: [tiles][kwin_ld] first staged (biased) bin
-  int kwin_ld = 0;
   FgGroup* groups = nullptr;  // angle groups of the grouped forward projector (active plan)
   int n_groups = 0;           // 0: geometry does not fit the grouped kernel -> k_fwd
   int fg_nkc = 0;             // grid.x of the grouped kernel: most chunks of any (group, segment)
@@ -318,8 +316,6 @@ int launch_back(admm_ctx* C, BackArgs<T> a, int V, hipStream_t s) {
   a.K = C->Kb;
   a.kbias = C->kbias;
   a.wexp = C->wexp;
-  a.kwin = (const int*)C->bkwin.p;
-  a.kwin_ld = C->kwin_ld;
   a.N = C->g.N;
   a.n_det = C->g.n_det;
   a.n_ang = C->g.n_angles;
@@ -712,34 +708,6 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
     const double kmn = C->Kb - c0 * (std::fabs(ba[t].Bi) + std::fabs(ba[t].Bj));
     C->kbias = std::max(C->kbias, (int)std::ceil(-kmn) + 2);
   }
-  // back-projector windows: for every (kBTJ x kBTI tile, angle) the first staged bin,
-  // floor(min k_f over the tile's corners) - 1 in the biased bin coordinate -- the same
-  // float64 formula (fma order) the kernel's taps use, so every tap lies in its window
-  {
-    const int gx = (g.N + kBTJ - 1) / kBTJ, gy = (g.N + kBTI - 1) / kBTI;
-    C->kwin_ld = (g.n_angles + 3) & ~3;
-    std::vector<int> kw((size_t)gx * gy * C->kwin_ld, 0);
-    const double Kc = C->Kb + (double)C->kbias;
-    for (int by = 0; by < gy; ++by)
-      for (int bx = 0; bx < gx; ++bx) {
-        const int ib = by * kBTI, jb = bx * kBTJ;
-        const int ihi = std::min(ib + kBTI - 1, g.N - 1), jhi = std::min(jb + kBTJ - 1, g.N - 1);
-        for (int t = 0; t < g.n_angles; ++t) {
-          auto kf = [&](int ii, int jj) {
-            return std::fma((double)ii - c0, bc[t].Bi, std::fma((double)jj - c0, bc[t].Bj, Kc));
-          };
-          const double kmn = std::fmin(std::fmin(kf(ib, jb), kf(ib, jhi)), std::fmin(kf(ihi, jb), kf(ihi, jhi)));
-          kw[((size_t)by * gx + bx) * C->kwin_ld + t] = (int)std::floor(kmn) - 1;
-        }
-      }
-    const int rc = ensure(C->bkwin, kw.size() * sizeof(int));
-    if (rc != ADMM_OK) {
-      const std::string msg = g_err;
-      admm_ctx_destroy(C);
-      return fail(rc, msg);
-    }
-    HIPCHK(hipMemcpy(C->bkwin.p, kw.data(), kw.size() * sizeof(int), hipMemcpyHostToDevice));
-  }
   if (C->wexp != 0) {  // exact power-of-two scaling (N < 3: L = 2 / (N |cos|) can exceed 1)
     for (int t = 0; t < g.n_angles; ++t) {
       bc[t].ws = float2v{std::ldexp(bc[t].ws.x, -C->wexp), std::ldexp(bc[t].ws.y, -C->wexp)};
@@ -943,7 +911,7 @@ int admm_ctx_destroy(admm_ctx* C) {
   free_graphs(C);
   Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->op_sino, &C->op_fpart, &C->op_order[0], &C->op_order[1], &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->bI, &C->fpart, &C->r, &C->c,
                  &C->d2, &C->e2, &C->partH, &C->partS, &C->partD, &C->partE, &C->redH, &C->fg_order, &C->dsumS, &C->ats,
-                 &C->f_ptr, &C->f_idx, &C->f_val, &C->t_ptr, &C->t_idx, &C->t_val, &C->x2, &C->p2, &C->pring, &C->bkwin};
+                 &C->f_ptr, &C->f_idx, &C->f_val, &C->t_ptr, &C->t_idx, &C->t_val, &C->x2, &C->p2, &C->pring};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   if (C->fang) (void)hipFree(C->fang);

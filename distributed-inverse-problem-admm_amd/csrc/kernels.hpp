@@ -904,8 +904,6 @@ struct BackArgs {
   const BackAngleC* angc;   // [n_ang] compact records
   double K;                 // angle-independent part of k_f
   int kbias;                // integer added to every k_f so that k_f > 0 (host: from the geometry)
-  const int* kwin;          // [tiles][kwin_ld]: first staged bin of each (tile, angle) window (biased)
-  int kwin_ld;              // row stride of kwin (angles rounded up to a multiple of 4)
   int wexp;                 // float weights of angc are scaled by 2^-wexp so that they are <= 1
   int N, n_det, n_ang, V;
   // explicit-matrix contexts (admm_ctx_create_matrix): A^T as CSR, one row per pixel
@@ -1207,6 +1205,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
   // the angle records are uniform -> scalar loads (shared table, scalar-cache resident)
   const double c0 = 0.5 * (N - 1);
   const double xi = (double)min(i, N - 1) - c0, yj = (double)min(j, N - 1) - c0;
+  const int jhi = min(jb + kBTJ - 1, N - 1), ihi = min(ib + kBTI - 1, N - 1);
   // bin positions are biased by an integer (admm_ctx: smallest k_f of any pixel, negated, + 2),
   // so k_f > 0: floor is the truncating convert and the tap fraction one v_fract_f64; window
   // offsets and the staged bins take the same bias
@@ -1217,18 +1216,15 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
   // window stays at 48 KB of LDS
   constexpr int ANGC = (NPL > 2) ? kBAngC / 2 : kBAngC;
   __shared__ Pack<T, PV> win[NPL][(MODE == BACK_WSQ) ? 1 : ANGC][kBWin];
-  // the first staged bin of this tile's window at every angle: a function of the geometry
-  // alone, tabulated at context creation (admm_ctx_create) -- so the first chunk's window
-  // loads issue at once, with no per-block window computation, LDS round trip or barrier
-  const int* kw_tile = A.kwin + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * A.kwin_ld;
+  __shared__ int4 kmin_s[2][ANGC / 4];  // per angle: window byte offset koff (see tap)
   T acc[VB];
 #pragma unroll
   for (int u = 0; u < VB; ++u) acc[u] = T(0);
   const T* sino_c = A.sino + (size_t)chunk * m_rays * VB;
   int t0c = 0;  // first angle of the current chunk (float64 weight path)
 
-  // window taps address LDS by byte offset: koff = (slot * kBWin - kwin) * sizeof(Pack) is formed
-  // once per angle on the scalar unit, so a tap's address is one v_lshl_add of k0
+  // window taps address LDS by byte offset: koff = (slot * kBWin - kmin) * sizeof(Pack) is formed
+  // once per angle and chunk (kmin_chunk), so a tap's address is one v_lshl_add of k0
   constexpr int PB = (int)sizeof(Pack<T, PV>);
   auto tap = [&](const BackAngleC& g, int koff, T& w0, T& w1, Pack<T, PV> (&s0)[NPL], Pack<T, PV> (&s1)[NPL],
                  int tt) {
@@ -1282,20 +1278,29 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
   // sinogram windows (MODE != WSQ).  PF: the next chunk's window is fetched into
   // registers before this chunk's taps and written to LDS after them (the single block per
   // CU otherwise waits for every chunk's loads with nothing to overlap; +12 VGPRs, still
-  // 4 waves/SIMD).  Otherwise: stage, tap per chunk.
+  // 4 waves/SIMD); kmin is double-buffered.  Otherwise: compute kmin, stage, tap per chunk.
   // (float samples, H/INIT modes: the float64 and DIAG variants would spill)
   constexpr bool PF = std::is_same<T, float>::value && (MODE == BACK_H || MODE == BACK_INIT ||
                                                                      MODE == BACK_PLAIN || MODE == BACK_ATB);
   constexpr int SPER = (ANGC * kBWin * NPL + kBkThreads - 1) / kBkThreads;
   Pack<T, PV> wst[SPER];
-  auto wfetch = [&](int t0) {
+  auto kmin_chunk = [&](int t0, int buf) {
+    const int nt = min(ANGC, n_ang - t0);
+    if ((int)threadIdx.x < nt) {
+      const BackAngleC g = A.angc[t0 + threadIdx.x];
+      auto kf = [&](int ii, int jj) { return fma((double)ii - c0, g.Bi, fma((double)jj - c0, g.Bj, Kc)); };
+      const double kmn = fmin(fmin(kf(ib, jb), kf(ib, jhi)), fmin(kf(ihi, jb), kf(ihi, jhi)));
+      reinterpret_cast<int*>(kmin_s[buf])[threadIdx.x] = ((int)threadIdx.x * kBWin - ((int)floor(kmn) - 1)) * PB;
+    }
+  };
+  auto wfetch = [&](int t0, int buf) {
     const int nt = min(ANGC, n_ang - t0);
 #pragma unroll
     for (int e = 0; e < SPER; ++e) {
       const int q = threadIdx.x + e * kBkThreads;
       const int pl = q % NPL, aw = q / NPL;
       const int a = aw / kBWin, w = aw - a * kBWin;
-      const int k = (a < nt) ? kw_tile[t0 + a] + w - kbias : -1;
+      const int k = (a < nt) ? a * kBWin - reinterpret_cast<const int*>(kmin_s[buf])[a] / PB + w - kbias : -1;
       if (a < nt && k >= 0 && k < n_det) {
         wst[e] = *reinterpret_cast<const Pack<T, PV>*>(sino_c + ((size_t)(t0 + a) * n_det + k) * VB + pl * PV);
       } else {
@@ -1332,17 +1337,23 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
     }
   }
   if constexpr (PF && !CSR) {
-    wfetch(0);
+    kmin_chunk(0, 0);
+    __syncthreads();
+    wfetch(0, 0);
     wcommit(0);
+    if (ANGC < n_ang) kmin_chunk(ANGC, 1);
     __syncthreads();
   }
-  for (int t0 = 0; !CSR && t0 < n_ang; t0 += ANGC) {
+  for (int t0 = 0, ci = 0; !CSR && t0 < n_ang; t0 += ANGC, ++ci) {
     const int nt = min(ANGC, n_ang - t0);
+    const int kb = (PF) ? (ci & 1) : 0;  // kmin buffer of this chunk
     if constexpr (PF) {
-      if (t0 + ANGC < n_ang) wfetch(t0 + ANGC);  // in flight during this chunk's taps
+      if (t0 + ANGC < n_ang) wfetch(t0 + ANGC, kb ^ 1);  // in flight during this chunk's taps
     } else if constexpr (MODE != BACK_WSQ) {
-      __syncthreads();  // the previous chunk's taps are done with win
-      wfetch(t0);
+      __syncthreads();
+      kmin_chunk(t0, 0);
+      __syncthreads();
+      wfetch(t0, 0);
       wcommit(t0);
       __syncthreads();
     }
@@ -1355,14 +1366,9 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
       BackAngleC g[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) g[u] = A.angc[t0 + tt + u];
-      int kms[4] = {0, 0, 0, 0};
-      if constexpr (MODE != BACK_WSQ) {
-        const int4 kw = *reinterpret_cast<const int4*>(kw_tile + t0 + tt);  // uniform: one scalar load
-        kms[0] = (tt * kBWin - kw.x) * PB;
-        kms[1] = ((tt + 1) * kBWin - kw.y) * PB;
-        kms[2] = ((tt + 2) * kBWin - kw.z) * PB;
-        kms[3] = ((tt + 3) * kBWin - kw.w) * PB;
-      }
+      int4 km = make_int4(0, 0, 0, 0);
+      if constexpr (MODE != BACK_WSQ) km = kmin_s[kb][tt >> 2];
+      const int kms[4] = {km.x, km.y, km.z, km.w};
 #pragma unroll
       for (int u = 0; u < 4; u += 2) {
         T wa0, wa1, wb0, wb1;
@@ -1376,7 +1382,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
     for (; tt < nt; ++tt) {
       const BackAngleC g = A.angc[t0 + tt];
       int km = 0;
-      if constexpr (MODE != BACK_WSQ) km = (tt * kBWin - kw_tile[t0 + tt]) * PB;
+      if constexpr (MODE != BACK_WSQ) km = reinterpret_cast<const int*>(kmin_s[kb])[tt];
       T wa0, wa1;
       Pack<T, PV> sa0[NPL], sa1[NPL];
       tap(g, km, wa0, wa1, sa0, sa1, tt);
@@ -1384,8 +1390,9 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
     }
     if constexpr (PF) {
       if (t0 + ANGC < n_ang) {
-        __syncthreads();  // this chunk's taps are done with win
+        __syncthreads();  // this chunk's taps are done with win and kmin_s[kb]
         wcommit(t0 + ANGC);
+        if (t0 + 2 * ANGC < n_ang) kmin_chunk(t0 + 2 * ANGC, kb);
         __syncthreads();
       }
     }
