@@ -117,3 +117,24 @@ def test_block5_and_block3_dropins_take_matrices(cuda, tmp_path):
     _, W3, _, keep = build_pixel_connected_Q_provider(str(tmp_path), "A_dense_list.npy", strategy="mst",
                                                       plot_union=False, verbose=False, show_plots=False)
     assert rel(np.stack(W3), np.stack(Wi)) < 2e-6 and tuple(keep.shape) == (V, V, N * N)
+
+
+def test_matrix_operator_sinograms_and_device_guard(cuda):
+    """make_sinograms on matrix operators (MatrixGeometry had no n_angles/n_det)
+    returns each node's m rows flat; applying an operator never changes the caller's
+    current device (the C entry points restore it)."""
+    N = 24
+    A = joseph_matrix(Geometry(N, 30)).tocsr()
+    op = MatrixOperator(A)
+    assert op.geom.n_angles == 1 and op.geom.n_det == A.shape[0]
+    ph = shepp_logan(N)
+    s = make_sinograms([op], ph, 0.0)[0]
+    assert tuple(s.shape) == (A.shape[0],)
+    assert rel(s.double().cpu().numpy(), A @ ph.numpy().ravel()) < 2e-6
+    before = torch.cuda.current_device()
+    for d in range(torch.cuda.device_count()):
+        from admm_hip.geometry import ParallelBeamGeometry, RayTransform
+        rt = RayTransform(ParallelBeamGeometry(N, 30), "float32", device=d)
+        _ = rt @ torch.ones(N * N, device=torch.device("cuda", d))
+        _ = rt.T @ torch.ones(30 * N, device=torch.device("cuda", d))
+        assert torch.cuda.current_device() == before, (d, before)
