@@ -6,7 +6,8 @@ BASELINE configs[2] exactly: 16 nodes, 1536 angles = 3N), lambda_TV = 0.02,
 rho = 2, split-Bregman 10 rounds x 5 CG steps per x-update, float32 projector
 samples / float64 solver state.  A "step" is one outer ADMM iteration: the
 x-update of every node, the halo exchange (RCCL), the z/y edge updates and the
-residual/statistics readback the reference's stop test needs.
+residual/statistics readback the reference's stop test needs (asynchronous, into pinned
+host memory: run_admm's pipelined mode).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--strong C4|none]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -254,16 +255,26 @@ def timed_steps(r, steps, warmup, world, prime=None):
     ranks).  ``prime(nb)`` runs right after the first x-update (before its exchange)."""
     import torch
     import torch.distributed as dist
-    from admm_hip.exchange import assemble_stats
+    from admm_hip.exchange import assemble_stats_device
     nb, halo, plan = r["nb"], r["halo"], r["plan"]
+    E = len(plan.stored_edges)
+    host = None
 
     def step(first=False):
+        nonlocal host
         nb.node_update()
         if first and prime is not None:
             prime(nb)
         halo.run()
         nb.consensus()
-        return assemble_stats(plan, nb.node_stats, nb.edge_stats[: len(plan.stored_edges)])
+        # the statistics the stop test reads (global table, RCCL all-reduce at N > 1), read
+        # back every step into pinned host memory without a per-step host synchronisation --
+        # run_admm's pipelined mode (the stop test cannot fire at eps = 0)
+        flat = assemble_stats_device(plan.V_total, len(plan.edges), world,
+                                     [(plan, nb.node_stats, nb.edge_stats[:E])])
+        if host is None:
+            host = torch.empty(flat.shape, dtype=flat.dtype, pin_memory=True)
+        host.copy_(flat, non_blocking=True)
 
     step(first=True)  # the first (full-projection) x-update; later ones replay the reuse graph
     for _ in range(max(0, warmup - 1)):

@@ -38,6 +38,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from .exchange import split_stats
 from .geometry import RayTransform
 from .groups import RankGroups
 from .matrix import MatrixOperator, as_operators
@@ -84,12 +85,16 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
              snapshot_every=None, snapshot_div=10, phantom_true=None, mu=None, tv_iters=10,
              cg_iters=5, tv_kind="iso", group=None, return_tensors=False, timing=None,
              write_params=True, fusion="midpoint", inner_tol=None, max_inner_updates=10,
-             inner_chunks=None, chunk_snapshot_dir=None, chunk_save_every=1, inspect=None):
+             inner_chunks=None, chunk_snapshot_dir=None, chunk_save_every=1, inspect=None,
+             pipeline=None):
     """``inner_chunks``: split each x-update into warm-started solves of these round counts
     (block_6_admm_loop.py:14-69 chunked SCS); ``chunk_snapshot_dir`` then receives that
     file's per-chunk snapshots (``_chunk_snapshot``) every ``chunk_save_every`` chunks.
     ``inspect(rg)``: called with the rank's device state (groups.RankGroups) after the loop
-    (tests check the edge invariants on the device arrays)."""
+    (tests check the edge invariants on the device arrays).  ``pipeline``: read the
+    statistics back once after the loop instead of every iteration (default: whenever the
+    stop test cannot fire and no per-iteration host output is requested; False forces the
+    per-iteration read-back)."""
     if inner_tol not in (None, "reference"):
         raise ValueError("inner_tol must be None (fixed counts) or 'reference'")
     if inner_chunks is not None:
@@ -133,6 +138,15 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
         import time
         t_loop = time.perf_counter()
     iters_done = 0
+    # Pipelined statistics: when the stop test cannot fire (eps_pri <= 0 or eps_dual <= 0:
+    # primal / dual are norms) and nothing else needs host values per iteration, each
+    # iteration's statistics table is assembled on the device (RCCL all-reduce at N > 1) into
+    # a row of a device history and read back once after the loop -- no host synchronisation
+    # per iteration, so the next iteration's launches queue behind the current one.  The
+    # histories are computed from the same values by the same host code (bitwise equal).
+    pipelined = ((eps_pri <= 0 or eps_dual <= 0) and inner_tol is None and snapshot_dir is None
+                 and chunk_snapshot_dir is None and pipeline is not False)
+    dev_hist = None
     for k in range(max_iters):
         et = eps_target(k)
         if inner_chunks is None:
@@ -150,44 +164,15 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
                 eps_used[rows], n_upd[rows] = _solve_to_reference_tolerance(nb, et, max_inner_updates)
         rg.exchange()
         rg.consensus()
-        ns, es = rg.stats(np.stack([eps_used, n_upd], axis=1))
-        ns = ns.numpy()
-        es = es.numpy()
         iters_done = k + 1
-        # --- node diagnostics (_ver2:145-206) ---
-        mse = ns[:, 0].copy()
-        g_norm = np.sqrt(ns[:, 1])
-        obj = 0.5 * ns[:, 0] + lam_tv * ns[:, 2] + ns[:, 3]
-        hist["g_norm_history"].append(g_norm)
-        hist["eps_used_history"].append(ns[:, 6].copy())
-        hist["eps_target_history"].append(np.full(V_total, et))
-        hist["sb_res_history"].append(np.sqrt(ns[:, 5]))
-        hist["inner_updates_history"].append(ns[:, 7].astype(np.int64))
-        hist["mse_sino_per_node"].append(mse)
-        hist["mse_sino_total"].append(float(np.sum(mse)))
-        img = ns[:, 4].copy() if have_ph else np.full(V_total, np.nan)
-        hist["img_mse_per_node"].append(img)
-        hist["img_mse_total"].append(float(np.sum(img)))
-        # --- residuals in G.edges() order (_ver2:232-258) ---
-        r2 = 0.0
-        s2 = 0.0
-        pri = np.zeros(V_total)
-        dua = np.zeros(V_total)
-        for ge, (a, b) in enumerate(edges):
-            ra2, rb2, dz2 = float(es[ge, 0]), float(es[ge, 1]), float(es[ge, 2])
-            r2 += ra2 + rb2
-            pri[a] += ra2
-            pri[b] += rb2
-            s2 += rho * rho * dz2
-            dua[a] += rho * rho * dz2
-            dua[b] += rho * rho * dz2
-        pn, dn = math.sqrt(r2), math.sqrt(s2)
-        hist["primal"].append(pn)
-        hist["dual"].append(dn)
-        hist["obj_per_node"].append(obj)
-        hist["obj_total"].append(float(np.sum(obj)))
-        hist["pri_per_node"].append(np.sqrt(pri))
-        hist["dual_per_node"].append(np.sqrt(dua))
+        if pipelined:
+            flat = rg.stats_device()
+            if dev_hist is None:
+                dev_hist = torch.empty((max_iters, flat.numel()), dtype=torch.float64, device=flat.device)
+            dev_hist[k].copy_(flat)
+            continue
+        ns, es = rg.stats(np.stack([eps_used, n_upd], axis=1))
+        pn, dn = _record(hist, ns.numpy(), es.numpy(), edges, V_total, rho, lam_tv, et, have_ph)
         if snapshot_dir is not None and ((k + 1) % snapshot_every == 0):
             _snapshot(snapshot_dir, k, rg, N)
         if verbose and rank == 0 and k % 10 == 0:
@@ -196,6 +181,16 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
             if verbose and rank == 0:
                 print(f"stopped at iter {k}, primal {pn:.3e}, dual {dn:.3e}")
             break
+    if pipelined and dev_hist is not None:
+        host = dev_hist[:iters_done].to("cpu")
+        nsw = rg.batches[0].node_stats.shape[1]
+        extra = np.stack([np.full(V_total, np.nan), np.ones(V_total)], axis=1)
+        for k in range(iters_done):
+            ns, es = split_stats(host[k], V_total, nsw, len(edges), rg.batches[0].edge_stats.shape[1])
+            pn, dn = _record(hist, np.concatenate([ns.numpy(), extra], axis=1), es.numpy(), edges, V_total,
+                             rho, lam_tv, eps_target(k), have_ph)
+            if verbose and rank == 0 and k % 10 == 0:
+                print(f"iter {k}, primal {pn:.3e}, dual {dn:.3e}")
     torch.cuda.synchronize()
     if timing is not None:
         import time
@@ -211,6 +206,46 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
         return [X[i] for i in range(V_total)], hist
     Xh = X.to("cpu").numpy()
     return [Xh[i].copy() for i in range(V_total)], hist
+
+
+def _record(hist, ns, es, edges, V_total, rho, lam_tv, et, have_ph):
+    """Append one iteration's histories from the global statistics tables (nodes x 8, edges x 3);
+    returns (primal, dual)."""
+    # --- node diagnostics (_ver2:145-206) ---
+    mse = ns[:, 0].copy()
+    g_norm = np.sqrt(ns[:, 1])
+    obj = 0.5 * ns[:, 0] + lam_tv * ns[:, 2] + ns[:, 3]
+    hist["g_norm_history"].append(g_norm)
+    hist["eps_used_history"].append(ns[:, 6].copy())
+    hist["eps_target_history"].append(np.full(V_total, et))
+    hist["sb_res_history"].append(np.sqrt(ns[:, 5]))
+    hist["inner_updates_history"].append(ns[:, 7].astype(np.int64))
+    hist["mse_sino_per_node"].append(mse)
+    hist["mse_sino_total"].append(float(np.sum(mse)))
+    img = ns[:, 4].copy() if have_ph else np.full(V_total, np.nan)
+    hist["img_mse_per_node"].append(img)
+    hist["img_mse_total"].append(float(np.sum(img)))
+    # --- residuals in G.edges() order (_ver2:232-258) ---
+    r2 = 0.0
+    s2 = 0.0
+    pri = np.zeros(V_total)
+    dua = np.zeros(V_total)
+    for ge, (a, b) in enumerate(edges):
+        ra2, rb2, dz2 = float(es[ge, 0]), float(es[ge, 1]), float(es[ge, 2])
+        r2 += ra2 + rb2
+        pri[a] += ra2
+        pri[b] += rb2
+        s2 += rho * rho * dz2
+        dua[a] += rho * rho * dz2
+        dua[b] += rho * rho * dz2
+    pn, dn = math.sqrt(r2), math.sqrt(s2)
+    hist["primal"].append(pn)
+    hist["dual"].append(dn)
+    hist["obj_per_node"].append(obj)
+    hist["obj_total"].append(float(np.sum(obj)))
+    hist["pri_per_node"].append(np.sqrt(pri))
+    hist["dual_per_node"].append(np.sqrt(dua))
+    return pn, dn
 
 
 def _solve_to_reference_tolerance(nb, et, max_inner_updates):

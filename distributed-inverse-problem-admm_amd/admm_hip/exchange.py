@@ -124,22 +124,53 @@ def assemble_stats_parts(V_total: int, E: int, world: int, parts, group=None):
         if E and plan0.stored_edges:
             edges[torch.tensor(plan0.stored_edges, dtype=torch.long)] = es0.detach().to("cpu")
         return nodes, edges
+    return split_stats(assemble_stats_device(V_total, E, world, parts, group).to("cpu"), V_total, ns, E, es)
+
+
+def assemble_stats_device(V_total: int, E: int, world: int, parts, group=None) -> torch.Tensor:
+    """The global statistics table of ``assemble_stats_parts`` left on the device, flat
+    ([V_total x ns | E x es] float64): stream-ordered, no host synchronisation (an RCCL
+    all-reduce at world > 1), for loops that read it back later (run_admm's pipelined mode,
+    bench.py).  ``split_stats`` cuts a host copy into the (nodes, edges) pair."""
+    plan0, ns0, es0 = parts[0]
+    ns = ns0.shape[1]
+    es = es0.shape[1] if es0 is not None else 3
     dev = ns0.device
+    if world == 1 and len(parts) == 1 and plan0.stored_edges == list(range(E)):
+        # one batch holding every node and every edge in G.edges() order: the table is its
+        # two statistics arrays back to back (one copy kernel)
+        return torch.cat([ns0.reshape(-1), es0[:E].reshape(-1)]) if E else ns0.reshape(-1).clone()
     buf = torch.zeros(V_total * ns + E * es, dtype=torch.float64, device=dev)
     nv = buf[: V_total * ns].view(V_total, ns)
     ev = buf[V_total * ns:].view(E, es)
     for plan, node_stats, edge_stats in parts:
         if plan.V:
-            nv.index_copy_(0, torch.tensor(plan.local_nodes, dtype=torch.long, device=dev), node_stats)
-        owned = [k for k, o in enumerate(plan.owned_edge) if o]
-        if owned:
-            slots = torch.tensor(owned, dtype=torch.long, device=dev)
-            gids = torch.tensor([plan.stored_edges[k] for k in owned], dtype=torch.long, device=dev)
-            ev.index_copy_(0, gids, edge_stats.index_select(0, slots))
+            nv.index_copy_(0, _index(plan, "local", dev), node_stats)
+        owned = _index(plan, "owned_slots", dev)
+        if owned.numel():
+            ev.index_copy_(0, _index(plan, "owned_gids", dev), edge_stats.index_select(0, owned))
     if world > 1:
         _all_reduce_sum(buf, group)
-    host = buf.to("cpu")
-    return host[: V_total * ns].view(V_total, ns), host[V_total * ns:].view(E, es)
+    return buf
+
+
+def split_stats(flat: torch.Tensor, V_total: int, ns: int, E: int, es: int):
+    return flat[: V_total * ns].view(V_total, ns), flat[V_total * ns:].view(E, es)
+
+
+def _index(plan: ShardPlan, what: str, dev) -> torch.Tensor:
+    """Device index tensors of a plan, built once (the statistics are assembled every
+    iteration)."""
+    cache = plan.__dict__.setdefault("_idx_cache", {})
+    key = (what, str(dev))
+    t = cache.get(key)
+    if t is None:
+        owned = [k for k, o in enumerate(plan.owned_edge) if o]
+        vals = {"local": plan.local_nodes, "owned_slots": owned,
+                "owned_gids": [plan.stored_edges[k] for k in owned]}[what]
+        t = torch.tensor(vals, dtype=torch.long, device=dev)
+        cache[key] = t
+    return t
 
 
 def gather_images(plan: ShardPlan, x_local: torch.Tensor, group=None) -> torch.Tensor:

@@ -25,7 +25,7 @@ from __future__ import annotations
 
 import torch
 
-from .exchange import HaloExchange, assemble_stats_parts, gather_images_parts
+from .exchange import HaloExchange, assemble_stats_device, assemble_stats_parts, gather_images_parts
 from .plan import ShardPlan, make_plan, make_subset_plan
 from .solver import NodeBatch
 
@@ -134,6 +134,12 @@ class RankGroups:
                 ns = torch.cat([ns, ex], dim=1)
             parts.append((nb.plan, ns, nb.edge_stats[: len(nb.plan.stored_edges)]))
         return assemble_stats_parts(self.plan.V_total, len(self.plan.edges), self.world, parts, self.group)
+
+    def stats_device(self) -> torch.Tensor:
+        """The global statistics table on the device (exchange.assemble_stats_device): no
+        host synchronisation."""
+        parts = [(nb.plan, nb.node_stats, nb.edge_stats[: len(nb.plan.stored_edges)]) for nb in self.batches]
+        return assemble_stats_device(self.plan.V_total, len(self.plan.edges), self.world, parts, self.group)
 
     def local_images(self):
         """[(global node, image row tensor)] of this rank's nodes, ascending."""

@@ -371,10 +371,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 
   const dim3 cgg((N + kTile - 1) / kTile, (N + kCgRows - 1) / kCgRows, nch);
   const int Pb = C->P_back;
 
-  // 0. D as interleaved samples for the CG operator (D is setup data; repacked per update)
-  hipLaunchKernelGGL((k_pack_d<T, VB>), dim3((unsigned)((npix + 255) / 256), nch), dim3(256), 0, s, B.dsum,
-                     (T*)C->dsumS.p, (int)npix, V);
-  CHECK_LAUNCH();
+  // (D as interleaved samples for the CG operator, dsumS, is packed once at bind time)
   if (reuse) {
     // 1-4. one kernel from the previous update's A^T (A xs - b) (ADMM_BATCH_KEEP_X):
     //      c, r = A^T b + rho c + mu K^T(d - e) - H x, p = r (+ transpose)
@@ -1050,6 +1047,21 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   RET(ensure(C->partE, (size_t)3 * std::max(1, B.n_edges) * C->P_edge * 8));
   RET(ensure(C->redH, (size_t)5 * V * 8 * std::max(1, std::min(B.cg_iters, kMaxCgRing))));
   C->bound = true;
+  // D = sum_j q_ij as interleaved samples of the sample dtype (the BACK_H epilogue's rho D p
+  // term): setup data, packed once here rather than in every x-update
+  RET(with_vb(C->vb, [&](auto vbc) {
+    constexpr int VB = decltype(vbc)::value;
+    const int nch = (V + VB - 1) / VB;
+    if (C->dtype == ADMM_DTYPE_F32)
+      hipLaunchKernelGGL((k_pack_d<float, VB>), dim3((unsigned)((npix + 255) / 256), nch), dim3(256), 0, C->cap,
+                         B.dsum, (float*)C->dsumS.p, (int)npix, V);
+    else
+      hipLaunchKernelGGL((k_pack_d<double, VB>), dim3((unsigned)((npix + 255) / 256), nch), dim3(256), 0, C->cap,
+                         B.dsum, (double*)C->dsumS.p, (int)npix, V);
+    CHECK_LAUNCH();
+    return ADMM_OK;
+  }));
+  HIPCHK(hipStreamSynchronize(C->cap));
   // the x-update and consensus sequences, recorded once and replayed every iteration
   auto fu = [&](hipStream_t s) {
     return C->dtype == ADMM_DTYPE_F32 ? enqueue_update_any<float>(C, s) : enqueue_update_any<double>(C, s);

@@ -112,7 +112,9 @@ typedef struct admm_batch {
     double* d;            /* [V][2][n]    split variable d ~ Kx (warm state)        */
     double* e;            /* [V][2][n]    Bregman variable (warm state)             */
     const double* atb;    /* [V][n]       A^T b                                     */
-    const double* dsum;   /* [V][n]       D_i = sum_j q_ij                          */
+    const double* dsum;   /* [V][n]       D_i = sum_j q_ij (setup data: also packed into the
+                           * CG operator's sample layout at admm_batch_bind -- rebind
+                           * after changing it)                                     */
     const void* b;        /* [V][m]       sinograms (context dtype)                 */
     const double* phantom;/* [n] or NULL  for ||x - phantom||^2                     */
 

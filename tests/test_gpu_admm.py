@@ -206,3 +206,20 @@ def test_build_node_problem_no_neighbours_no_tv(cuda):
     r0 = np.linalg.norm(b)
     r1 = np.linalg.norm(A @ xi.value - b)
     assert r1 < 0.1 * r0
+
+
+def test_pipelined_statistics_equal_per_iteration_readback(cuda):
+    """run_admm's pipelined mode (eps = 0: the stop test cannot fire, statistics read back
+    once after the loop) gives bitwise the histories and images of the per-iteration
+    read-back; with the 5-node unequal-angle split (two batches) as well."""
+    from admm_hip.admm import run_admm
+    for V, angles in ((4, 96 * 4), (5, 192)):
+        ops, ph, sinos, Wi, Q, A, _ = setup_problem(48, V, angles)
+        G = nx.cycle_graph(V)
+        runs = [run_admm(ops, sinos, G, Wi, Q, 48, lam_tv=0.02, rho=2.0, max_iters=4, eps_pri=0.0,
+                         eps_dual=0.0, verbose=False, phantom_true=ph, write_params=False, pipeline=pl)
+                for pl in (None, False)]
+        (x1, h1), (x2, h2) = runs
+        assert all(np.array_equal(a, b) for a, b in zip(x1, x2))
+        for k in h1:
+            assert np.array_equal(np.asarray(h1[k]), np.asarray(h2[k]), equal_nan=True), k
