@@ -76,7 +76,12 @@ int ensure(Buf& b, size_t bytes) {
   b.bytes = 0;
   if (bytes == 0) return ADMM_OK;
   HIPCHK(hipMalloc(&b.p, bytes));
+  // hipMemset is enqueued on the null stream, which does not order against non-blocking
+  // streams (the capture stream, a caller's torch stream): finish the zero-fill before any
+  // kernel can write the buffer (measured: the bind-time D packing on the capture stream
+  // was overwritten by its own buffer's zero-fill)
   HIPCHK(hipMemset(b.p, 0, bytes));
+  HIPCHK(hipDeviceSynchronize());
   b.bytes = bytes;
   return ADMM_OK;
 }
