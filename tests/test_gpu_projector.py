@@ -148,3 +148,22 @@ def test_fullsize_column_norm_point_symmetry(cuda):
     W = RayTransform(ParallelBeamGeometry(N, 96)).column_norms_sq().reshape(N, N)
     assert np.all(W > 0)
     assert rel(W, W[::-1, ::-1]) < 1e-5
+
+
+def test_operator_first_use_on_a_side_stream(cuda):
+    """A context's scratch is allocated and zero-filled on first use; the zero-fill (null
+    stream) must be complete before kernels on a caller's non-blocking stream write the
+    scratch (a fresh geometry, so every buffer is allocated inside the stream scope)."""
+    N, a = 56, 33
+    g = ParallelBeamGeometry(N, a)
+    rng = np.random.default_rng(4)
+    X = torch.as_tensor(rng.standard_normal((5, N * N)), dtype=torch.float32, device=cuda)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        Y = RayTransform(g, "float32") @ X
+        Z = RayTransform(g, "float32").T @ Y
+    s.synchronize()
+    Yd = RayTransform(g, "float32") @ X
+    Zd = RayTransform(g, "float32").T @ Yd
+    torch.cuda.synchronize()
+    assert torch.equal(Y, Yd) and torch.equal(Z, Zd)
