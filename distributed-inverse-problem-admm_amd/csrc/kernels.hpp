@@ -96,45 +96,6 @@ struct alignas((VB * sizeof(T)) >= 16 ? 16 : (VB * sizeof(T))) Pack {
   T v[VB];
 };
 
-// Stores of outputs the NEXT launch reads, optionally write-through (cache policy sc1: the
-// line leaves the XCD's L2 at once instead of being written back while the next kernel waits
-// at the dependent-launch boundary).  `base` must be uniform (a kernel argument), `idx` the
-// element index from it; N contiguous elements of T (4, 8, 16, 32 or 64 bytes).
-#ifndef ADMM_WT_STORES
-#define ADMM_WT_STORES 0
-#endif
-template <typename T, int N>
-__device__ __forceinline__ void ostore(T* __restrict__ base, size_t idx, const T (&v)[N]) {
-  if constexpr (!ADMM_WT_STORES) {
-#pragma unroll
-    for (int u = 0; u < N; ++u) base[idx + u] = v[u];
-  } else {
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-    constexpr int B = N * (int)sizeof(T);
-    constexpr int SC1 = 16;  // gfx950 cache policy bits: 1 = sc0, 2 = nt, 16 = sc1
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
-    const int off = (int)(idx * sizeof(T));
-    if constexpr (B % 16 == 0) {
-#pragma unroll
-      for (int q = 0; q < B / 16; ++q) {
-        u32x4 d;
-        __builtin_memcpy(&d, reinterpret_cast<const char*>(v) + 16 * q, 16);
-        __builtin_amdgcn_raw_buffer_store_b128(d, r, off + 16 * q, 0, SC1);
-      }
-    } else if constexpr (B == 8) {
-      u32x2 d;
-      __builtin_memcpy(&d, v, 8);
-      __builtin_amdgcn_raw_buffer_store_b64(d, r, off, 0, SC1);
-    } else {
-      static_assert(B == 4, "4, 8 or a multiple of 16 bytes");
-      unsigned int d;
-      __builtin_memcpy(&d, v, 4);
-      __builtin_amdgcn_raw_buffer_store_b32(d, r, off, 0, SC1);
-    }
-  }
-}
-
 template <typename T, int VB>
 struct Planes {
   static constexpr int BYTES = VB * (int)sizeof(T);
@@ -866,7 +827,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   }
   if (g < G && k >= 0 && k < n_det) {
     const size_t m_rays = (size_t)n_ang * n_det;
-    ostore<T, VB>(part, (((size_t)seg * ((V + VB - 1) / VB) + chunk) * m_rays + (size_t)t * n_det + k) * VB, acc);
+    gstore<T, VB>(part + (((size_t)seg * ((V + VB - 1) / VB) + chunk) * m_rays + (size_t)t * n_det + k) * VB, acc);
   }
 }
 
@@ -906,7 +867,7 @@ __global__ __launch_bounds__(kBlock) void k_fwd_combine(const T* __restrict__ pa
         }
       }
     }
-    ostore<T, VB>(sino, ((size_t)chunk * m_rays + ray) * VB, acc);
+    gstore<T, VB>(sino + ((size_t)chunk * m_rays + ray) * VB, acc);
   }
   if (MODE == 1) {
     __shared__ double lds[4 * VB];
@@ -1097,7 +1058,7 @@ __device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j
         }
       }
     }
-    ostore<T, VB>(A.out_t, sbase + (size_t)pix * VB, outv);
+    gstore<T, VB>(A.out_t + sbase + (size_t)pix * VB, outv);
   }  // BACK_DIAG: diag_epilogue_tile (block-cooperative)
 }
 
@@ -1692,12 +1653,12 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(double* __restrict__ x, do
         const double pd = (double)pv[u];
         if constexpr (WRITE_X) x[o] = fma(alpha, pd, x[o]);  // (explicit fma: k_tv_update<FUSE> repeats it bitwise)
         const double rn = fma(-alpha, (double)hv[u], r[o]);
-        ostore<double, 1>(r, o, {rn});
+        r[o] = rn;
         np[u] = (T)(rn + beta * pd);
       }
       if constexpr (WRITE_P) tl[ii][jj][u] = np[u];
     }
-    if constexpr (WRITE_P) ostore<T, VB>(pout, sbase + (size_t)pix * VB, np);
+    if constexpr (WRITE_P) gstore<T, VB>(pout + sbase + (size_t)pix * VB, np);
   }
   if constexpr (!WRITE_P) return;
   __syncthreads();
@@ -1705,7 +1666,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(double* __restrict__ x, do
   const int u = threadIdx.x % VB, rr_ = (threadIdx.x / VB) % kCgRows, c0 = threadIdx.x / (VB * kCgRows);
   for (int c = c0; c < kTile; c += kBlock / (VB * kCgRows)) {
     const int jc = j0 + c, ic = i0 + rr_;
-    if (jc < N && ic < N) ostore<T, 1>(pT, sbase + ((size_t)jc * N + ic) * VB + u, {tl[rr_][c][u]});
+    if (jc < N && ic < N) pT[sbase + ((size_t)jc * N + ic) * VB + u] = tl[rr_][c][u];
   }
 }
 
