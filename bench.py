@@ -205,7 +205,7 @@ def cpu_baseline(N, a, b, q, x_gpu, procs=None, budget=CPU_BASELINE_SECONDS):
 # summary (scripts/pmc.sh + scripts/traffic_summary.py over the launches between the
 # bench's markers, i.e. the timed steps; 2 x FETCH_SIZE + WRITE_SIZE per the
 # MI355X_MICROARCH.md gfx950 correction).  PMC counters cannot be read inside this run.
-TRAFFIC_FILE = "profiles/r2_traffic.json"
+TRAFFIC_FILE = "profiles/r3_traffic.json"
 FWD_KERNEL = "admm::k_fwdg<float, 8>"
 
 
