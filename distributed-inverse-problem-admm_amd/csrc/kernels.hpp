@@ -1214,7 +1214,11 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
 
   // angles per staged chunk: halved for 64-B sample vectors (8 float64 nodes) so the
   // window stays at 48 KB of LDS
-  constexpr int ANGC = (NPL > 2) ? kBAngC / 2 : kBAngC;
+  // (the DIAG epilogue's tile scratch needs LDS too: its windows stay within 96 KB)
+  constexpr int ANGC_ = (NPL > 2) ? kBAngC / 2 : kBAngC;
+  constexpr int ANGC_DIAG = (98304 / (NPL * kBWin * (int)sizeof(Pack<T, PV>))) & ~3;
+  constexpr int ANGC = (MODE == BACK_DIAG && ANGC_ > ANGC_DIAG) ? ANGC_DIAG : ANGC_;
+  static_assert(ANGC % 4 == 0, "angle chunks are read as int4 groups");
   __shared__ Pack<T, PV> win[NPL][(MODE == BACK_WSQ) ? 1 : ANGC][kBWin];
   __shared__ int4 kmin_s[2][ANGC / 4];  // per angle: window byte offset koff (see tap)
   T acc[VB];
