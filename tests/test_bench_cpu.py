@@ -1,4 +1,4 @@
-"""CPU: bench.py's launch decision (driver contract).
+"""CPU: bench.py's launch decision (driver contract), its CPU leg and the C4 graph fixture.
 
 * ``--gpus N`` under a launcher must equal WORLD_SIZE (an error, not a warning);
 * without a launcher and N > 1, bench.py starts the N ranks itself and fails when a rank
@@ -50,3 +50,19 @@ def test_cpu_baseline_reports_eq1_certificate():
     c = r["eq1_gap"]
     assert c["m"] > 0 and c["dist_bound"] > 0 and c["obj_gap_bound"] >= c["eps"] >= 0
     assert c["dist_bound"] >= c["stationarity"] / c["m"]
+
+
+def test_c4_graph_matches_committed_adjacency():
+    """C4's Erdos-Renyi graph (32 nodes, p = 2 ln 32 / 32, seed 0, resampled
+    until connected) is committed as a fixture; bench.make_graph must reproduce it exactly
+    (a networkx change in the generator would silently change the C4 workload)."""
+    import json
+    import networkx as nx
+    sys.path.insert(0, ROOT)
+    from bench import make_graph
+    with open(os.path.join(ROOT, "tests", "golden", "c4_er32_graph.json")) as f:
+        fx = json.load(f)
+    G = make_graph("er", 32)
+    assert G.number_of_nodes() == fx["nodes"] == 32 and nx.is_connected(G)
+    assert sorted([list(e) for e in G.edges()]) == fx["edges"]
+    assert len(fx["edges"]) == 103
