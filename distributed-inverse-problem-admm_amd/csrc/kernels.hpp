@@ -488,9 +488,10 @@ constexpr int kFgSeg = ADMM_FG_SEG;    // row segments (partial sums) per ray
 #ifndef ADMM_FG_DMA_ROWS
 #define ADMM_FG_DMA_ROWS 2  // rows per chunk of the LDS-DMA kernel (4: 34.7 us, 1: 38.0 us at 512^2 vs 32.5)
 #endif
-constexpr int kFgHalf = kFgWin / 2;        // slots per parity
-constexpr int kFgOdd = kFgHalf + 4;        // odd half-window offset (+64 B bank shift)
-constexpr int kFgRow = kFgOdd + kFgHalf;   // 16-B slots per staged row and plane
+constexpr int kFgHalf = kFgWin / 2;                // slots per parity
+constexpr int kFgPieces = (kFgHalf + 63) / 64;     // 64-slot LDS-DMA pieces per parity half
+constexpr int kFgOdd = 64 * kFgPieces + 4;         // odd half-window offset (+64 B bank shift)
+constexpr int kFgRow = kFgOdd + 64 * kFgPieces;    // 16-B slots per staged row and plane
 
 // ray (within a 64-ray chunk) of each lane: ds_read_b128 lane groups -> 16 consecutive rays
 __device__ __forceinline__ int fg_ray_of_lane(int lane) {
@@ -556,7 +557,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   // 2-row chunk of taps ahead; 4-row chunks, or a 3/4-buffer ring with counted vmcnt waits
   // keeping 2-3 chunks in flight, measured slower)
   constexpr int R = kDma ? ADMM_FG_DMA_ROWS : kFgRows;
-  constexpr int PIECES = NPL * R * 4;  // 1-KiB LDS-DMA pieces per chunk
+  constexpr int PIECES = NPL * R * 2 * kFgPieces;  // 1-KiB LDS-DMA pieces per chunk
   __shared__ Pack<T, PV> win[kDma ? 2 : 1][NPL][R][kFgRow];
   // every row window of the segment (N <= 4096): origin and the width actually touched
   __shared__ __align__(16) int wlo_s[(4096 + kFgSeg - 1) / kFgSeg + 4];  // +4: int4 reads of the last chunk
@@ -732,7 +733,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
     auto dma = [&](int m0, int b) {
       const int rows = min(R, m_hi - m0);
       for (int q = g; q < PIECES; q += kFgG) {  // wave-uniform
-        const int h = q & 1, par = (q >> 1) & 1, rp = q >> 2;
+        const int h = q % kFgPieces, par = (q / kFgPieces) & 1, rp = q / (2 * kFgPieces);
         const int r = rp % R, pl = rp / R;
         if (r >= rows) continue;
         const int wo = __builtin_amdgcn_readfirstlane(wlo_s[m0 - m_lo + r]);
