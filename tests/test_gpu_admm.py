@@ -49,7 +49,7 @@ def node_weights(Wi, seed=5):
 
 
 def compare(G, N, V, iters, angles_total, dtype="float32", tol=1e-5, tv_kind="iso", lam=0.02,
-            rho=2.0, tv_iters=10, cg_iters=5, fusion="midpoint"):
+            rho=2.0, tv_iters=10, cg_iters=5, fusion="midpoint", g_tol=None):
     ops, ph, sinos, Wi, Q, A, sin_h = setup_problem(N, V, angles_total, dtype)
     Wo = None
     if fusion == "weighted":
@@ -77,7 +77,7 @@ def compare(G, N, V, iters, angles_total, dtype="float32", tol=1e-5, tv_kind="is
         assert errs[k] < max(10 * tol, 1e-4), (k, errs)
     # |g| contains the TV subgradient K^T(Kx/|Kx|), discontinuous where |Kx| ~ 0 (flat
     # phantom regions): image differences of 1e-7 move it by ~1e-5.  Diagnostic only.
-    assert errs["g"] < max(20 * tol, 2e-4), errs  # measured <= 2.4e-5 (C1, 20 iterations)
+    assert errs["g"] < (g_tol or max(20 * tol, 2e-4)), errs  # measured <= 2.4e-5 (C1, 20 iterations)
     return x, h, xo, ho
 
 
@@ -128,6 +128,28 @@ def test_ragged_image_and_node_chunks(cuda):
     """N = 37 (partial 32-pixel tiles everywhere) and V = 11 (one full 8-node chunk and a
     ragged 3-node one) through the whole loop."""
     compare(nx.cycle_graph(11), 37, 11, 4, 11 * 20)
+
+
+def test_isolated_node_matches_oracle(cuda):
+    """A node with no neighbours (deg 0: D = 0, c = 0, its x-update is the TV-regularised
+    least-squares problem alone; _ver2:85-97 with an empty neighbour list)."""
+    G = nx.path_graph(3)
+    G.add_node(3)
+    # the isolated node's |g| is its TV subgradient term alone (no consensus pull): 2e-6
+    # image differences move it by 3e-4 there (measured), so its diagnostic bar is 1e-3
+    compare(G, 32, 4, 4, 96, g_tol=1e-3)
+
+
+def test_graph_without_edges_matches_oracle(cuda):
+    """E = 0: every node independent, residuals identically zero (_ver2:232-289 over no
+    edges), statistics table of node rows only."""
+    G = nx.empty_graph(3)
+    x, h, xo, ho = compare(G, 24, 3, 3, 72)
+    assert np.all(np.asarray(h["primal"]) == 0) and np.all(np.asarray(h["dual"]) == 0)
+
+
+def test_single_node_matches_oracle(cuda):
+    compare(nx.empty_graph(1), 32, 1, 3, 48)
 
 
 def test_cg_steps_beyond_the_direction_ring(cuda):
