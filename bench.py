@@ -398,8 +398,13 @@ def main():
     value = V_total * args.steps / el
     ms_per_step = 1e3 * el / args.steps
 
-    # live measurement of the dominant kernel (forward projector taps) on its stream
-    fwd_ms = nb.time_forward(args.fwd_reps)
+    # live measurement of the dominant kernel (forward projector taps) on its stream: HIP events
+    # around every CG-step forward of one more x-update (after the timed region and the halo
+    # check), each launch right after the CG / TV update that wrote its image, as in the timed
+    # steps -- the figure rocprofv3's in-solve average must agree with; back-to-back launches,
+    # which find the image rows still in L2, are reported beside it
+    fwd_ms = nb.time_forward(in_solve=True)
+    fwd_ms_warm = nb.time_forward(args.fwd_reps)
     a_node = geom.n_angles
     sbytes = 8 if dtype == "float64" else 4
     B_A, B_At, B_node = sample_touch_bytes(n_img, a_node, TV_ITERS, CG_ITERS, sbytes)
@@ -433,13 +438,15 @@ def main():
         "traffic_source": (f"{TRAFFIC_FILE}: rocprofv3 PMC 2 x FETCH_SIZE + WRITE_SIZE per in-solve "
                            "launch (Infinity-Cache hits included)") if fwd_traffic is not None else None,
         "avg_launch_ms": fwd_ms,
+        "avg_launch_ms_back_to_back": fwd_ms_warm,
         "compulsory_bytes": compulsory,
         "compulsory_frac": compulsory / fwd_s / 1e9 / HBM_PEAK_GBS,
         "as_designed_bytes": as_designed,
         "traffic_over_compulsory": fwd_traffic / compulsory if fwd_traffic is not None else None,
         "sample_touch_bytes": B_A * V,
         "reuse_factor": B_A * V / compulsory,
-        "note": "frac = PMC bytes per launch / live event-timed duration / 8 TB/s. compulsory = each "
+        "note": "frac = PMC bytes per launch / live event-timed duration of the in-solve launches (HIP "
+                "events around each CG-step forward of one x-update) / 8 TB/s. compulsory = each "
                 "node image read once + its sinogram written once; as_designed adds the transposed "
                 "image copy (case-A angles) and the 8 segment partials. sample_touch (SURVEY 8d) "
                 "counts every tap as a 4-byte load; taps are LDS reads, so it is a reuse factor, "

@@ -198,9 +198,11 @@ class NodeBatch:
                                          C.c_void_p(self._mk[1].data_ptr()), 1, C.c_void_p(self._s())),
                    "admm_tv_grad")
 
-    def time_forward(self, reps: int = 20) -> float:
+    def time_forward(self, reps: int = 20, in_solve: bool = False) -> float:
+        """Average k_fwdg launch (ms): ``reps`` back-to-back, or ``in_solve`` -- every CG-step
+        forward of one directly enqueued x-update (the batch's state advances by it)."""
         ms = C.c_double()
-        _lib.check(self.lib.admm_time_forward(self.ctx.h, reps, C.c_void_p(self._s()), C.byref(ms)),
+        _lib.check(self.lib.admm_time_forward(self.ctx.h, reps, int(in_solve), C.c_void_p(self._s()), C.byref(ms)),
                    "admm_time_forward")
         return ms.value
 

@@ -136,6 +136,10 @@ struct admm_ctx {
   Buf x2, p2; // ping-pong partners of x (local rows) and p for the fused TV update
   Buf pring;  // CG direction slots 1 .. K-1 (direction ring; slot 0 = p, slot K = p2)
   Buf ats;    // A^T (A xs - b) of the last update's final x (ADMM_BATCH_KEEP_X)
+  // admm_time_forward(in_solve): events around every CG-step forward tap launch of one
+  // directly enqueued x-update (null outside that measurement)
+  std::vector<hipEvent_t>* tf_ev = nullptr;
+  size_t tf_next = 0;
   bool ats_valid = false;  // ats matches x_ext's local rows
   hipGraph_t g_update_reuse = nullptr;
   hipGraphExec_t x_update_reuse = nullptr;
@@ -303,10 +307,22 @@ int launch_fwdg_taps(admm_ctx* C, const T* img, const T* imgT, int V, hipStream_
 
 template <typename T, int VB, int MODE>
 int launch_fwd_batch(admm_ctx* C, const T* img, const T* imgT, T* sino, const T* b, double* part, int V,
-                     hipStream_t s) {
-  if (C->n_groups == 0) return launch_fwd<T, VB, MODE>(C, img, imgT, sino, b, part, V, s);
+                     hipStream_t s, bool timed = false) {
+  // timed (admm_time_forward in_solve): HIP events right before and after the tap kernel
+  hipEvent_t* ev = nullptr;
+  if (timed && C->tf_ev && C->tf_next + 2 <= C->tf_ev->size()) {
+    ev = C->tf_ev->data() + C->tf_next;
+    C->tf_next += 2;
+    HIPCHK(hipEventRecord(ev[0], s));
+  }
+  if (C->n_groups == 0) {
+    RET((launch_fwd<T, VB, MODE>(C, img, imgT, sino, b, part, V, s)));
+    if (ev) HIPCHK(hipEventRecord(ev[1], s));
+    return ADMM_OK;
+  }
   const int nch = (V + VB - 1) / VB;
   RET((launch_fwdg_taps<T, VB>(C, img, imgT, V, s)));
+  if (ev) HIPCHK(hipEventRecord(ev[1], s));
   dim3 cg((C->mrays + kBlock - 1) / kBlock, nch);
   hipLaunchKernelGGL((k_fwd_combine<T, VB, MODE>), cg, dim3(kBlock), 0, s, (const T*)C->fpart.p, sino, b, part,
                      C->fang, C->g.n_det, C->g.n_angles, V);
@@ -438,7 +454,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 
     for (int kk = 0; kk < K; ++kk) {
       T* pk = (F == 2) ? slot[kk] : slot[0];
       double* rk = redH + kk * rstride;
-      RET((launch_fwd_batch<T, VB, 0>(C, pk, pT, sino, nullptr, nullptr, V, s)));
+      RET((launch_fwd_batch<T, VB, 0>(C, pk, pT, sino, nullptr, nullptr, V, s, true)));
       BackArgs<T> a{};
       a.sino = sino;
       a.out_t = Hp;
@@ -1158,38 +1174,70 @@ int admm_consensus(admm_ctx* C, void* stream) {
 
 extern "C++" {
 template <typename T>
-int time_fwd(admm_ctx* C, int reps, hipStream_t s, float* ms) {
-  return with_vb(C->vb, [&](auto vbc) {
+int time_fwd(admm_ctx* C, int reps, int in_solve, hipStream_t s, float* ms) {
+  return with_vb(C->vb, [&](auto vbc) -> int {
     constexpr int VB = decltype(vbc)::value;
-    hipEvent_t e0, e1;
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    // the dominant kernel alone: k_fwdg (every sample tap) when grouped, else k_fwd
+    if (in_solve) {
+      // one x-update enqueued directly (the graph's launch sequence, no graph), with events
+      // around each CG step's forward tap launch: the predecessor is the CG / TV update that
+      // just wrote p and p^T, exactly as in every replay
+      const int n = C->b.tv_iters * C->b.cg_iters;
+      std::vector<hipEvent_t> ev(2 * n);
+      // timing-only events: no system-scope fence (cache writeback / invalidation) at each
+      // record, which would perturb the launches they bracket
+      for (auto& e : ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+      C->tf_ev = &ev;
+      C->tf_next = 0;
+      const bool keep = (C->b.flags & ADMM_BATCH_KEEP_X) != 0;
+      int rc = enqueue_update<T, VB>(C, s, keep && C->ats_valid);
+      const size_t used = C->tf_next;
+      C->tf_ev = nullptr;
+      if (rc == ADMM_OK && keep) C->ats_valid = true;
+      if (rc == ADMM_OK && used == 0) rc = fail(ADMM_E_STATE, "no forward launch was timed");
+      if (rc == ADMM_OK) {
+        HIPCHK(hipEventSynchronize(ev[used - 1]));
+        float tot = 0.f;
+        for (size_t i = 0; i < used; i += 2) {
+          float t = 0.f;
+          HIPCHK(hipEventElapsedTime(&t, ev[i], ev[i + 1]));
+          tot += t;
+        }
+        *ms = tot / (float)(used / 2);
+      }
+      for (auto& e : ev) (void)hipEventDestroy(e);
+      return rc;
+    }
+    // the dominant kernel alone, back to back: k_fwdg (every sample tap) when grouped, else k_fwd
     auto one = [&]() -> int {
       if (C->n_groups > 0) return launch_fwdg_taps<T, VB>(C, (T*)C->xs.p, (T*)C->xsT.p, C->b.V, s);
       return launch_fwd<T, VB, 0>(C, (T*)C->xs.p, (T*)C->xsT.p, (T*)C->sino.p, nullptr, nullptr, C->b.V, s);
     };
     RET(one());
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreateWithFlags(&e0, hipEventDisableSystemFence));
+    HIPCHK(hipEventCreateWithFlags(&e1, hipEventDisableSystemFence));
     HIPCHK(hipEventRecord(e0, s));
-    for (int i = 0; i < reps; ++i) RET(one());
+    int rc = ADMM_OK;
+    for (int i = 0; i < reps && rc == ADMM_OK; ++i) rc = one();
     HIPCHK(hipEventRecord(e1, s));
     HIPCHK(hipEventSynchronize(e1));
     HIPCHK(hipEventElapsedTime(ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    return ADMM_OK;
+    return rc;
   });
 }
 }  // extern "C++"
 
-int admm_time_forward(admm_ctx* C, int reps, void* stream, double* ms_out) {
+int admm_time_forward(admm_ctx* C, int reps, int in_solve, void* stream, double* ms_out) {
   if (!C || !C->bound) return fail(ADMM_E_STATE, "no batch bound");
   if (reps < 1 || !ms_out) return fail(ADMM_E_INVALID, "bad argument");
   DEVICE_SCOPE(C->device);
   hipStream_t s = (hipStream_t)stream;
   float ms = 0.f;
-  RET(C->dtype == ADMM_DTYPE_F32 ? time_fwd<float>(C, reps, s, &ms) : time_fwd<double>(C, reps, s, &ms));
-  *ms_out = (double)ms / reps;
+  RET(C->dtype == ADMM_DTYPE_F32 ? time_fwd<float>(C, reps, in_solve, s, &ms)
+                                  : time_fwd<double>(C, reps, in_solve, s, &ms));
+  *ms_out = in_solve ? (double)ms : (double)ms / reps;
   return ADMM_OK;
 }
 

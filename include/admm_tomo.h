@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ADMM_ABI_VERSION 4
+#define ADMM_ABI_VERSION 5
 
 #define ADMM_OK 0
 #define ADMM_E_INVALID (-1)
@@ -195,11 +195,17 @@ int admm_node_update_rounds(admm_ctx* ctx, int tv_iters, void* stream);
  * into edge_stats.  Replaces block_6_admm_loop_ver2.py:210-253.  Every edge
  * slot of the batch is processed; x_ext halo rows must be current. */
 int admm_consensus(admm_ctx* ctx, void* stream);
-/* Average duration (ms) of `reps` back-to-back launches of the forward
- * projector's tap kernel (k_fwdg, which makes every sample tap; its segment
- * partial sums are not combined) on the bound batch's current x, timed with HIP
- * events on `stream`.  Measurement helper for bench.py; synchronises. */
-int admm_time_forward(admm_ctx* ctx, int reps, void* stream, double* ms_out);
+/* Average duration (ms) of a launch of the forward projector's tap kernel (k_fwdg,
+ * which makes every sample tap; its segment partial sums are not combined) on the
+ * bound batch, timed with HIP events on `stream`.
+ * in_solve = 0: `reps` back-to-back launches on the batch's current x (the image
+ *   rows stay in L2 from one launch to the next).
+ * in_solve = 1 (ABI 5): one x-update of the bound batch is enqueued directly (the
+ *   launch sequence its graph replays) with events around each CG step's forward
+ *   tap launch -- right after the CG / TV update that wrote p and p^T, as in every
+ *   solve; the batch's state advances by that x-update.  `reps` is ignored.
+ * Measurement helper for bench.py; synchronises. */
+int admm_time_forward(admm_ctx* ctx, int reps, int in_solve, void* stream, double* ms_out);
 
 /* --- per-pixel edge masks for masked precisions (setup) --- */
 
