@@ -83,3 +83,24 @@ def test_fullsize_single_node_update_vs_oracle(problem):
                     ons.NodeParams(rho=2.0, lam=0.02, mu=0.2, tv_iters=2, cg_iters=3))
     x = nb.x_ext[0].cpu().numpy()
     assert np.linalg.norm(x - st.x) / np.linalg.norm(st.x) < 1e-5
+
+
+def test_in_solve_forward_timing_runs_the_graph_sequence(problem):
+    """bench.py's forward timing (admm_time_forward in_solve) enqueues one x-update directly
+    with events around its CG-step forwards: the state it leaves is bitwise the state the
+    recorded graph's replay leaves, and the per-launch time is a positive launch duration."""
+    ops, ph, sinos, Wi, Q = problem
+    G = nx.cycle_graph(V)
+    plan = make_plan(G, V)
+    mk = lambda: NodeBatch(ops[0].geom, "float32", plan, sinos, Q, 2.0, 0.02, 0.2, 10, 5, "iso", ph, 0,  # noqa: E731
+                           keep_x=True)
+    a, b = mk(), mk()
+    for nb in (a, b):  # one ordinary update each, so the next one takes the start-reuse path
+        nb.node_update()
+    a.node_update()
+    ms = b.time_forward(in_solve=True)
+    torch.cuda.synchronize()
+    assert 0.005 < ms < 1.0, ms  # ~0.03 ms at this size
+    assert torch.equal(a.x_ext, b.x_ext)
+    assert torch.equal(a.node_stats, b.node_stats)
+    assert 0.005 < b.time_forward(7) < 1.0
