@@ -206,6 +206,20 @@ class NodeBatch:
                    "admm_time_forward")
         return ms.value
 
+    def fwd_plans(self) -> list[dict]:
+        """The grouped forward projector's plans for this batch's geometry (admm_fwd_plan_info):
+        per plan 0/1/2 its angle groups, blocks per node chunk, staged row pixels (host model)
+        and whether it is the bound one; plans the geometry does not have are omitted."""
+        out = []
+        for pl in range(3):
+            g, b, a, st = C.c_int(), C.c_int(), C.c_int(), C.c_double()
+            _lib.check(self.lib.admm_fwd_plan_info(self.ctx.h, pl, C.byref(g), C.byref(b), C.byref(st),
+                                                   C.byref(a)), "admm_fwd_plan_info")
+            if g.value:
+                out.append(dict(plan=pl, groups=g.value, blocks=b.value, staged_px=st.value,
+                                active=bool(a.value)))
+        return out
+
 
 def make_operators(N: int, num_nodes: int, angles_total: int | None = None, dtype: str = "float32",
                    device: int | None = None, det_width_factor: float = 1.0) -> list[RayTransform]:

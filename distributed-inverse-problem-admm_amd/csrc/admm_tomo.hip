@@ -105,12 +105,16 @@ struct admm_ctx {
   int kbias = 0;    // integer bias making every pixel's k_f positive (k_back)
   int wexp = 0;     // k_back float weights scaled by 2^-wexp (<= 1 for the fma clamp)
   FgGroup* groups = nullptr;  // angle groups of the grouped forward projector (active plan)
+  FgRange* rng = nullptr;     // its per-block ray ranges
   int n_groups = 0;           // 0: geometry does not fit the grouped kernel -> k_fwd
-  int fg_nkc = 0;             // grid.x of the grouped kernel: most chunks of any (group, segment)
-  // the two group plans (0: unaligned, 1: ray-aligned per row segment), chosen at bind time
-  FgGroup* plan_groups[2] = {nullptr, nullptr};
-  int plan_n[2] = {0, 0}, plan_nkc[2] = {0, 0}, plan_blocks[2] = {0, 0};
-  std::vector<FgGroup> plan_host[2];  // host copies (block table construction)
+  // the group plans (0: 64-ray chunks, 1: chunks aligned per (row segment, angle) at the
+  // detector centre, 2: chunks aligned per (row segment, chunk)), chosen at bind time
+  static constexpr int kPlans = 3;
+  FgGroup* plan_groups[kPlans] = {};
+  FgRange* plan_rng[kPlans] = {};
+  int plan_n[kPlans] = {}, plan_blocks[kPlans] = {};
+  double plan_staged[kPlans] = {};      // touched row pixels staged per node chunk (host model)
+  std::vector<int4> plan_blk[kPlans];  // per block: {ray-range index, group, segment, G}
   Buf fg_order;                       // int4 block table of the grouped forward projector
   int fg_nblk = 0, fg_order_nch = 0;
   hipStream_t cap = nullptr;  // private capture stream
@@ -124,8 +128,8 @@ struct admm_ctx {
   // operator-API scratch (admm_project_fwd runs the hot grouped kernel on up to 8 images
   // per launch: node-major images packed into the interleaved sample layout)
   Buf op_img, op_imgT, op_sino, op_fpart;
-  Buf op_order[2];  // block tables of the two forward plans for one node chunk
-  int op_nblk[2] = {0, 0};
+  Buf op_order[kPlans];  // block tables of the forward plans for one node chunk
+  int op_nblk[kPlans] = {};
 
   // batch
   bool bound = false;
@@ -164,8 +168,8 @@ int vb_for(int V) { return V >= 5 ? 8 : (V >= 3 ? 4 : (V == 2 ? 2 : 1)); }
 
 void select_fwd_plan(admm_ctx* C, int pl) {
   C->groups = C->plan_groups[pl];
+  C->rng = C->plan_rng[pl];
   C->n_groups = C->plan_n[pl];
-  C->fg_nkc = C->plan_nkc[pl];
 }
 
 // Block table of the grouped forward projector for nch node chunks: every live
@@ -179,11 +183,8 @@ int build_fwd_order_into(admm_ctx* C, int pl, int nch, int cus, Buf& buf, int* n
     int w;
   };
   std::vector<Blk> v;
-  const auto& gv = C->plan_host[pl];
   for (int c = 0; c < nch; ++c)
-    for (int gi = 0; gi < (int)gv.size(); ++gi)
-      for (int s = 0; s < kFgSeg; ++s)
-        for (int kc = 0; kc < gv[gi].nkc[s]; ++kc) v.push_back({make_int4(kc, gi, s + kFgSeg * c, 0), gv[gi].G});
+    for (const int4& b : C->plan_blk[pl]) v.push_back({make_int4(b.x, b.y, b.z + kFgSeg * c, 0), b.w});
   const int n = (int)v.size();
   auto by_weight = [](std::vector<Blk>& l, int slots) {
     std::stable_sort(l.begin(), l.end(), [](const Blk& a, const Blk& b) { return a.w > b.w; });
@@ -231,7 +232,9 @@ int build_fwd_order(admm_ctx* C, int pl, int nch, int cus) {
 // Forward plan for the bound batch: the ray-aligned plan stages less per tap but has one
 // more chunk per (group, segment); take it unless the busiest CU would host more of its
 // blocks (e.g. 512^2: 512 unaligned blocks put 2 on every one of 256 CUs, the aligned 528
-// put 3 on some; co-resident blocks share the CU).  ADMM_FWD_PLAN=0/1 forces a plan.
+// put 3 on some; co-resident blocks share the CU).  The chunk-aligned plan (2) replaces it
+// when it stages fewer pixels without more blocks per CU (large images: 2048^2 stages half
+// the pixels of plan 1 in 2/3 of its blocks).  ADMM_FWD_PLAN=0/1/2 forces a plan.
 // (The occupancy query only guards against a plan that cannot be resident at all.)
 template <typename T, int VB>
 int pick_fwd_plan(admm_ctx* C, int nch, int* pl_out, int* cus_out) {
@@ -241,8 +244,9 @@ int pick_fwd_plan(admm_ctx* C, int nch, int* pl_out, int* cus_out) {
   if (per_cu < 1) return fail(ADMM_E_HIP, "grouped forward projector cannot be resident");
   auto per_cu_max = [&](int pl) { return ((long)C->plan_blocks[pl] * nch + cus - 1) / std::max(1, cus); };
   int pl = per_cu_max(1) <= per_cu_max(0) ? 1 : 0;
+  if (C->plan_n[2] > 0 && per_cu_max(2) <= per_cu_max(pl) && C->plan_staged[2] < C->plan_staged[pl]) pl = 2;
   const char* f = getenv("ADMM_FWD_PLAN");
-  if (f && (f[0] == '0' || f[0] == '1')) pl = f[0] - '0';
+  if (f && f[0] >= '0' && f[0] <= '2' && C->plan_n[f[0] - '0'] > 0) pl = f[0] - '0';
   *pl_out = pl;
   *cus_out = cus;
   return ADMM_OK;
@@ -290,9 +294,9 @@ int launch_fwd(admm_ctx* C, const T* img, const T* imgT, T* sino, const T* b, do
 // the grouped forward projector's tap kernel (all sample taps; segment partials -> fpart)
 template <typename T, int VB>
 int launch_fwdg_taps_with(admm_ctx* C, const T* img, const T* imgT, T* fpart, const FgGroup* groups,
-                          const int4* order, int nblk, int V, hipStream_t s) {
-  hipLaunchKernelGGL((k_fwdg<T, VB>), dim3(nblk), dim3(kFgThreads), 0, s, img, imgT, fpart, C->fang, groups, order,
-                     C->g.N, C->g.n_det, C->g.n_angles, V);
+                          const FgRange* rng, const int4* order, int nblk, int V, hipStream_t s) {
+  hipLaunchKernelGGL((k_fwdg<T, VB>), dim3(nblk), dim3(kFgThreads), 0, s, img, imgT, fpart, C->fang, groups, rng,
+                     order, C->g.N, C->g.n_det, C->g.n_angles, V);
   CHECK_LAUNCH();
   return ADMM_OK;
 }
@@ -301,8 +305,8 @@ template <typename T, int VB>
 int launch_fwdg_taps(admm_ctx* C, const T* img, const T* imgT, int V, hipStream_t s) {
   const int nch = (V + VB - 1) / VB;
   if (nch != C->fg_order_nch) return fail(ADMM_E_STATE, "forward block table built for another batch size");
-  return launch_fwdg_taps_with<T, VB>(C, img, imgT, (T*)C->fpart.p, C->groups, (const int4*)C->fg_order.p,
-                                      C->fg_nblk, V, s);
+  return launch_fwdg_taps_with<T, VB>(C, img, imgT, (T*)C->fpart.p, C->groups, C->rng,
+                                      (const int4*)C->fg_order.p, C->fg_nblk, V, s);
 }
 
 template <typename T, int VB, int MODE>
@@ -622,7 +626,7 @@ int op_forward_chunk(admm_ctx* C, const T* img, T* sino, int nc, hipStream_t s) 
   CHECK_LAUNCH();
   hipLaunchKernelGGL((k_transpose<T, VB>), tile_grid(C, 1, VB), dim3(kBlock), 0, s, (const T*)xs, xsT, C->g.N);
   CHECK_LAUNCH();
-  RET((launch_fwdg_taps_with<T, VB>(C, xs, xsT, (T*)C->op_fpart.p, C->plan_groups[pl],
+  RET((launch_fwdg_taps_with<T, VB>(C, xs, xsT, (T*)C->op_fpart.p, C->plan_groups[pl], C->plan_rng[pl],
                                     (const int4*)C->op_order[pl].p, C->op_nblk[pl], nc, s)));
   hipLaunchKernelGGL((k_fwd_combine<T, VB, 0>), dim3((m + kBlock - 1) / kBlock, 1), dim3(kBlock), 0, s,
                      (const T*)C->op_fpart.p, sI, (const T*)nullptr, (double*)nullptr, C->fang, C->g.n_det,
@@ -733,54 +737,127 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
     }
   }
   // angle groups for the grouped forward projector: consecutive angles of one case,
-  // G <= kFgG, whose union row window of every 64-ray chunk fits kFgWin (float64, same
-  // formulas as the device; 2 pixels of margin).  Two plans: plain 64-ray chunks, and rays
-  // aligned per row segment (FgGroup.delta: narrower windows and larger groups, at the
-  // price of one more chunk per segment); admm_batch_bind picks one (fewer block rounds).
-  std::vector<FgGroup> groups_plan[2];
+  // G <= kFgG, whose union row window of every block fits kFgWin (float64, same formulas as
+  // the device; 2 pixels of margin).  Three plans, each a table of per-block ray ranges
+  // (FgRange): plain 64-ray chunks; 64-ray chunks aligned per (row segment, angle) at the
+  // detector centre (FgGroup.delta: narrower windows and larger groups, one more chunk per
+  // segment); chunks aligned per (row segment, chunk) -- every angle's chunk x starts at the
+  // same pixel of the segment's centre row, so windows stay narrow far from the detector
+  // centre, where the rays' spacing 1/|cos| differs between the group's angles.
+  // admm_batch_bind picks one (pick_fwd_plan).
+  constexpr int kPlans = admm_ctx::kPlans;
+  std::vector<FgGroup> groups_plan[kPlans];
+  std::vector<FgRange> rng_plan[kPlans];
+  std::vector<int4> blk_plan[kPlans];
+  double staged_plan[kPlans] = {};
   bool fits = true;
-  int plan_nkc[2] = {0, 0}, plan_blocks[2] = {0, 0};
   {
     const double cd = 0.5 * (g.n_det - 1);
-    auto plan_group = [&](int t0, int G, bool align, FgGroup& gr) -> bool {
+    // touched row pixels of one block over its segment's rows, -1 if a row is too wide
+    auto window_px = [&](int t0, int G, int mlo, int mhi, const FgRange& r) -> long {
+      long px = 0;
+      for (int m = mlo; m < mhi; ++m) {
+        double lo = 1e300, hi = -1e300;
+        for (int q = 0; q < G; ++q) {
+          if (r.nk[q] == 0) continue;
+          const FwdAngle& b = fa[t0 + q];
+          for (int kk : {r.k0[q], r.k0[q] + r.nk[q] - 1}) {
+            const double l = std::fma((double)m, b.dl, std::fma((double)kk, b.A1, b.A0));
+            lo = std::min(lo, l);
+            hi = std::max(hi, l);
+          }
+        }
+        if (lo > hi) continue;
+        const double w = std::floor(hi) - std::floor(lo) + 2;
+        if (w > kFgWin - 2) return -1;
+        px += (long)w;
+      }
+      return px;
+    };
+    // the blocks of group (t0, G) under plan pl: ray ranges rv, block entries bv
+    // ({range index within rv, group index gi, segment, G}), staged pixels st
+    auto plan_group = [&](int t0, int G, int pl, int gi, FgGroup& gr, std::vector<FgRange>& rv,
+                          std::vector<int4>& bv, double& st) -> bool {
       for (int q = 0; q < G; ++q)
         if (fa[t0 + q].caseA != fa[t0].caseA) return false;
       gr = FgGroup{};
       gr.t0 = t0;
       gr.G = G;
+      rv.clear();
+      bv.clear();
+      st = 0.0;
       for (int s = 0; s < kFgSeg; ++s) {
         const int mlo = s * g.N / kFgSeg, mhi = (s + 1) * g.N / kFgSeg;
         const double mc = 0.5 * (mlo + mhi - 1);
-        const FwdAngle& r0 = fa[t0];
-        const double lref = r0.A0 + cd * r0.A1 + mc * r0.dl;  // reference ray at the centre row
-        int dmin = 0, dmax = 0;
-        for (int q = 0; q < G; ++q) {
-          const FwdAngle& b = fa[t0 + q];
-          const int d = align ? (int)std::lround((lref - b.A0 - cd * b.A1 - mc * b.dl) / b.A1) : 0;
-          gr.delta[s][q] = d;
-          dmin = std::min(dmin, d);
-          dmax = std::max(dmax, d);
-        }
-        const int kcb = (int)std::floor(-dmax / 64.0);
-        const int kce = (int)std::ceil((g.n_det - dmin) / 64.0);
-        gr.kcb[s] = kcb;
-        gr.nkc[s] = kce - kcb;
-        for (int kc = kcb; kc < kce; ++kc) {
-          for (int m = mlo; m < mhi; ++m) {
-            double lo = 1e300, hi = -1e300;
+        auto emit = [&](const FgRange& r) -> bool {
+          bool any = false;
+          for (int q = 0; q < G; ++q) any = any || r.nk[q] > 0;
+          if (!any) return true;
+          const long px = window_px(t0, G, mlo, mhi, r);
+          if (px < 0) return false;
+          st += (double)px;
+          bv.push_back(make_int4((int)rv.size(), gi, s, G));
+          rv.push_back(r);
+          return true;
+        };
+        if (pl < 2) {
+          const FwdAngle& r0 = fa[t0];
+          const double lref = r0.A0 + cd * r0.A1 + mc * r0.dl;  // reference ray at the centre row
+          int dmin = 0, dmax = 0;
+          for (int q = 0; q < G; ++q) {
+            const FwdAngle& b = fa[t0 + q];
+            const int d = pl == 1 ? (int)std::lround((lref - b.A0 - cd * b.A1 - mc * b.dl) / b.A1) : 0;
+            gr.delta[s][q] = d;
+            dmin = std::min(dmin, d);
+            dmax = std::max(dmax, d);
+          }
+          const int kcb = (int)std::floor(-dmax / 64.0);
+          const int kce = (int)std::ceil((g.n_det - dmin) / 64.0);
+          gr.kcb[s] = kcb;
+          gr.nkc[s] = kce - kcb;
+          for (int kc = kcb; kc < kce; ++kc) {
+            FgRange r{};
             for (int q = 0; q < G; ++q) {
-              const FwdAngle& b = fa[t0 + q];
-              const int ka = std::max(kc * 64 + gr.delta[s][q], 0);
-              const int kb = std::min(kc * 64 + gr.delta[s][q] + 63, g.n_det - 1);
-              if (ka > kb) continue;
-              for (int kk : {ka, kb}) {
-                const double l = std::fma((double)m, b.dl, std::fma((double)kk, b.A1, b.A0));
-                lo = std::min(lo, l);
-                hi = std::max(hi, l);
-              }
+              const int lo = std::max(kc * 64 + gr.delta[s][q], 0);
+              const int hi = std::min(kc * 64 + gr.delta[s][q] + 64, g.n_det);
+              r.k0[q] = lo;
+              r.nk[q] = std::max(0, hi - lo);
             }
-            if (lo > hi) continue;
-            if (std::floor(hi) - std::floor(lo) + 2 > kFgWin - 2) return false;
+            if (!emit(r)) return false;
+          }
+        } else {
+          // position of ray k at the centre row, along the direction of increasing k:
+          // u_q(k) = sgn (A0 + mc dl) + k |A1|; chunk x holds the rays with u in
+          // [U0 + x S, U0 + (x + 1) S), S = 64 min|A1| (<= 64 rays of every angle)
+          const double sgn = fa[t0].A1 > 0 ? 1.0 : -1.0;
+          double amin = 1e300, U0 = 1e300;
+          double cq[kFgG], aq[kFgG];
+          for (int q = 0; q < G; ++q) {
+            const FwdAngle& b = fa[t0 + q];
+            if ((b.A1 > 0) != (sgn > 0)) return false;
+            aq[q] = std::fabs(b.A1);
+            cq[q] = sgn * (b.A0 + mc * b.dl);
+            amin = std::min(amin, aq[q]);
+            U0 = std::min(U0, cq[q]);
+          }
+          const double S = 64.0 * amin * (1.0 - 1e-9);
+          auto bnd = [&](int q, long x) {
+            const double v = std::ceil((U0 + (double)x * S - cq[q]) / aq[q]);
+            return (int)std::min(std::max(v, 0.0), (double)g.n_det);
+          };
+          for (long x = 0;; ++x) {
+            if (x > 4L * g.n_det + 8) return false;  // (cannot happen: every chunk spans >= 64 pixels)
+            FgRange r{};
+            bool done = true;
+            for (int q = 0; q < G; ++q) {
+              const int lo = bnd(q, x), hi = bnd(q, x + 1);
+              done = done && lo >= g.n_det;
+              r.k0[q] = std::min(lo, g.n_det - 1);
+              r.nk[q] = hi - lo;
+              if (r.nk[q] > 64) return false;
+            }
+            if (done) break;
+            if (!emit(r)) return false;
           }
         }
       }
@@ -789,20 +866,25 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
     // greedy: the largest G <= kFgG consecutive same-case angles whose windows fit.
     // (Balanced splits of each same-case run were measured slower: they force wide windows
     // near 45 degrees, where greedy makes small narrow groups and stages fewer pixels.)
-    for (int pl = 0; pl < 2 && fits; ++pl) {
+    for (int pl = 0; pl < kPlans && fits; ++pl) {
       for (int t0 = 0; t0 < g.n_angles;) {
         int G = std::min(kFgG, g.n_angles - t0);
+        const int gi = (int)groups_plan[pl].size();
         FgGroup gr{};
-        while (G > 1 && !plan_group(t0, G, pl == 1, gr)) --G;
-        if (G == 1 && !plan_group(t0, 1, pl == 1, gr)) {
-          fits = false;
+        std::vector<FgRange> rv;
+        std::vector<int4> bv;
+        double st = 0.0;
+        while (G > 1 && !plan_group(t0, G, pl, gi, gr, rv, bv, st)) --G;
+        if (G == 1 && !plan_group(t0, 1, pl, gi, gr, rv, bv, st)) {
+          if (pl < 2) fits = false;  // no grouped kernel for this geometry
+          groups_plan[pl].clear();   // (plan 2 is optional)
           break;
         }
+        const int base = (int)rng_plan[pl].size();
+        for (int4 b : bv) blk_plan[pl].push_back(make_int4(b.x + base, b.y, b.z, b.w));
+        rng_plan[pl].insert(rng_plan[pl].end(), rv.begin(), rv.end());
         groups_plan[pl].push_back(gr);
-        for (int s = 0; s < kFgSeg; ++s) {
-          plan_nkc[pl] = std::max(plan_nkc[pl], gr.nkc[s]);
-          plan_blocks[pl] += gr.nkc[s];
-        }
+        staged_plan[pl] += st;
         t0 += G;
       }
     }
@@ -818,14 +900,18 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
   HIPCHK(hipMalloc(&C->bangc, bc.size() * sizeof(BackAngleC)));
   HIPCHK(hipMemcpy(C->bangc, bc.data(), bc.size() * sizeof(BackAngleC), hipMemcpyHostToDevice));
   if (fits) {
-    for (int pl = 0; pl < 2; ++pl) {
+    for (int pl = 0; pl < kPlans; ++pl) {
       const auto& gv = groups_plan[pl];
+      const auto& rv = rng_plan[pl];
+      if (gv.empty()) continue;
       HIPCHK(hipMalloc(&C->plan_groups[pl], gv.size() * sizeof(FgGroup)));
       HIPCHK(hipMemcpy(C->plan_groups[pl], gv.data(), gv.size() * sizeof(FgGroup), hipMemcpyHostToDevice));
-      C->plan_host[pl] = gv;
+      HIPCHK(hipMalloc(&C->plan_rng[pl], rv.size() * sizeof(FgRange)));
+      HIPCHK(hipMemcpy(C->plan_rng[pl], rv.data(), rv.size() * sizeof(FgRange), hipMemcpyHostToDevice));
+      C->plan_blk[pl] = blk_plan[pl];
       C->plan_n[pl] = (int)gv.size();
-      C->plan_nkc[pl] = plan_nkc[pl];
-      C->plan_blocks[pl] = plan_blocks[pl];
+      C->plan_blocks[pl] = (int)blk_plan[pl].size();
+      C->plan_staged[pl] = staged_plan[pl];
     }
     select_fwd_plan(C, 0);  // until a batch is bound
   }
@@ -937,6 +1023,8 @@ int admm_ctx_destroy(admm_ctx* C) {
   if (C->bangc) (void)hipFree(C->bangc);
   for (FgGroup* pg : C->plan_groups)
     if (pg) (void)hipFree(pg);
+  for (FgRange* pr : C->plan_rng)
+    if (pr) (void)hipFree(pr);
   if (C->cap) (void)hipStreamDestroy(C->cap);
   delete C;
   return ADMM_OK;
@@ -1238,6 +1326,16 @@ int admm_time_forward(admm_ctx* C, int reps, int in_solve, void* stream, double*
   RET(C->dtype == ADMM_DTYPE_F32 ? time_fwd<float>(C, reps, in_solve, s, &ms)
                                   : time_fwd<double>(C, reps, in_solve, s, &ms));
   *ms_out = in_solve ? (double)ms : (double)ms / reps;
+  return ADMM_OK;
+}
+
+int admm_fwd_plan_info(admm_ctx* C, int plan, int* groups, int* blocks, double* staged, int* active) {
+  if (!C || plan < 0 || plan >= admm_ctx::kPlans || !groups || !blocks || !staged || !active)
+    return fail(ADMM_E_INVALID, "bad argument");
+  *groups = C->plan_n[plan];
+  *blocks = C->plan_blocks[plan];
+  *staged = C->plan_staged[plan];
+  *active = (C->plan_n[plan] > 0 && C->groups == C->plan_groups[plan]) ? 1 : 0;
   return ADMM_OK;
 }
 

@@ -511,6 +511,17 @@ struct FgGroup {
   int nkc[kFgSeg];          // chunks of each row segment
   int delta[kFgSeg][kFgG];  // per-angle ray offsets
 };
+// The rays one block projects: angle t0+q of its group takes rays k0[q] .. k0[q]+nk[q]-1
+// (0 <= nk <= 64, inside [0, n_det)).  Every plan is a table of these (one per (group,
+// segment, chunk)); per (group, segment) the ranges of each angle partition its rays.  The
+// fixed-chunk plans give every angle rays (kcb+x)*64 + delta + [0, 64) clipped to the
+// detector; the chunk-aligned plan starts every angle's chunk x at the same pixel of the
+// segment's centre row (a chunk spans 64 rays of the group's densest angle, so sparser
+// angles use fewer lanes), which keeps the union window narrow far from the detector centre.
+struct FgRange {
+  int k0[kFgG];
+  int nk[kFgG];
+};
 
 #ifndef ADMM_FG_WPE
 #define ADMM_FG_WPE 8  // waves per SIMD the register budget must allow: <= 64 VGPRs, 2 blocks/CU
@@ -519,26 +530,26 @@ struct FgGroup {
 template <typename T, int VB>
 __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM_FG_WPE))) void k_fwdg(const T* __restrict__ img, const T* __restrict__ imgT,
                                                  T* __restrict__ part, const FwdAngle* __restrict__ ang,
-                                                 const FgGroup* __restrict__ groups, const int4* __restrict__ order,
-                                                 int N, int n_det, int n_ang, int V) {
+                                                 const FgGroup* __restrict__ groups, const FgRange* __restrict__ rng,
+                                                 const int4* __restrict__ order, int N, int n_det, int n_ang, int V) {
   constexpr int NPL = Planes<T, VB>::NPL, PV = Planes<T, VB>::PV;
   constexpr int PER = (kFgRows * kFgWin * NPL + kFgThreads - 1) / kFgThreads;  // staged packs per thread
   // g (the wave's angle slot) is wave-uniform: readfirstlane lets the compiler keep it, and
   // everything derived from it (group offsets, DMA piece indices, the idle test), in SGPRs
   // with scalar branches instead of VALU compares and EXEC masking
   const int lane = threadIdx.x & 63, g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  // 1-D grid over a host-ordered block table (order[b] = {chunk of rays, group, seg +
+  // 1-D grid over a host-ordered block table (order[b] = {ray ranges, group, seg +
   // kFgSeg * node chunk}): heavy (large-G) blocks first, paired with light ones on a CU
   const int4 ob = order[blockIdx.x];
-  const int bkc = ob.x;
+  const FgRange* rg = rng + ob.x;
   const FgGroup* gr = groups + ob.y;
   const int seg = ob.z % kFgSeg, chunk = ob.z / kFgSeg;
-  if (bkc >= gr->nkc[seg]) return;  // block-uniform, before any barrier (never in the table)
   const int G = gr->G, t0 = gr->t0;
-  const int kbase = (gr->kcb[seg] + bkc) * 64;
   const int npix = N * N;
   const int gq = min(g, G - 1);
-  const int k = kbase + gr->delta[seg][gq] + fg_ray_of_lane(lane);
+  // lanes past the angle's range repeat its last ray (taps inside the window, store masked)
+  const int nkq = rg->nk[gq], rl = fg_ray_of_lane(lane);
+  const int k = rg->k0[gq] + min(rl, nkq - 1);
   const int kcl = clampi(k, 0, n_det - 1);
   const int t = t0 + gq;
   const FwdAngle a = ang[t];
@@ -575,7 +586,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   }
   __syncthreads();
   if (g < G) {  // wave-uniform; a == ang[t0 + g] here
-    const int ka = max(kbase + gr->delta[seg][g], 0), kb = min(kbase + gr->delta[seg][g] + 63, n_det - 1);
+    const int ka = rg->k0[g], kb = rg->k0[g] + rg->nk[g] - 1;
     if (ka <= kb) {
       const double ca = fma((double)ka, a.A1, a.A0), cb = fma((double)kb, a.A1, a.A0);
       for (int r = lane; r < nrows; r += 64) {
@@ -724,7 +735,8 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   };
   // waves g >= G (groups smaller than kFgG) only stage and meet the barriers: their taps
   // would repeat angle G-1's and burn the LDS bandwidth the real taps are bound by
-  const bool idle = g >= G;
+  // (and waves whose angle has no rays in this block)
+  const bool idle = g >= G || nkq == 0;
 
   if constexpr (kDma) {
     // one 1-KiB piece per wave-instruction: 64 consecutive 16-B slots of one (plane, row,
@@ -826,7 +838,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       taps(win[0], m0, idle ? 0 : min(R, m_hi - m0), wl);
     }
   }
-  if (g < G && k >= 0 && k < n_det) {
+  if (g < G && rl < nkq) {
     const size_t m_rays = (size_t)n_ang * n_det;
     gstore<T, VB>(part + (((size_t)seg * ((V + VB - 1) / VB) + chunk) * m_rays + (size_t)t * n_det + k) * VB, acc);
   }

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ADMM_ABI_VERSION 5
+#define ADMM_ABI_VERSION 6
 
 #define ADMM_OK 0
 #define ADMM_E_INVALID (-1)
@@ -206,6 +206,13 @@ int admm_consensus(admm_ctx* ctx, void* stream);
  *   solve; the batch's state advances by that x-update.  `reps` is ignored.
  * Measurement helper for bench.py; synchronises. */
 int admm_time_forward(admm_ctx* ctx, int reps, int in_solve, void* stream, double* ms_out);
+/* ABI 6: the grouped forward projector's plan `plan` (0: 64-ray chunks, 1: chunks aligned
+ * per (row segment, angle) at the detector centre, 2: chunks aligned per (row segment,
+ * chunk)) for this context's geometry: angle groups, blocks per node chunk, touched row
+ * pixels staged per node chunk (the host planner's model), and active = 1 if it is the plan
+ * the bound batch (or, before a bind, the context) uses.  groups = 0: no such plan.
+ * No device work.  (Tests and tuning; the plans give bitwise-identical projections.) */
+int admm_fwd_plan_info(admm_ctx* ctx, int plan, int* groups, int* blocks, double* staged, int* active);
 
 /* --- per-pixel edge masks for masked precisions (setup) --- */
 

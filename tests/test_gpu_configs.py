@@ -117,7 +117,7 @@ def test_c3_two_ranks_match_one_rank_bitwise(cuda):
         assert np.array_equal(np.asarray(h1["primal"]), pr) and np.array_equal(np.asarray(h1["dual"]), du)
 
 
-@pytest.mark.timeout(400)
+@pytest.mark.timeout(600)
 @pytest.mark.parametrize("N,V,dtype,tv,graph,tvi,tol", [
     (1024, 8, "float32", "iso", "ring", 10, 1e-5),        # C4 size (8 of its 32 nodes per GPU)
     (2048, 4, "float64", "aniso", "complete", 4, 1e-9),   # C5 size, precision and TV
@@ -126,11 +126,12 @@ def test_large_x_updates_match_operator_oracle(cuda, monkeypatch, N, V, dtype, t
     ops, ph, sinos, Wi, Q = problem(N, V, 96, dtype)
     G = nx.cycle_graph(V) if graph == "ring" else nx.complete_graph(V)
     runs = []
-    for plan in ("0", "1"):
+    for plan in ("0", "1", "2"):
         monkeypatch.setenv("ADMM_FWD_PLAN", plan)
         runs.append(gpu_run(ops, sinos, G, Wi, Q, N, 2, ph, tv_kind=tv, tv_iters=tvi))
     monkeypatch.delenv("ADMM_FWD_PLAN")
-    assert np.array_equal(runs[0][0], runs[1][0]) and runs[0][1]["primal"] == runs[1][1]["primal"]
+    for xr, hr in runs[1:]:
+        assert np.array_equal(runs[0][0], xr) and runs[0][1]["primal"] == hr["primal"]
     x, h = runs[1]
     sin_h = [s.double().cpu().numpy() for s in sinos]
     xo, ho = oadmm.decentralized_admm(ops, sin_h, G, Q, N, lam_tv=0.02, rho=2.0, max_iters=2,

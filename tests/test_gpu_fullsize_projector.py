@@ -6,7 +6,8 @@ layout, VB = 1/2/4/8 by image count).  The oracle is the float64 Joseph CSR
 matrix of oracle/geometry.py restricted to a handful of angles per case (the
 full matrix is ~2.4 GB at 1024^2 and ~10 GB at 2048^2): both sides of the
 45-degree case switch, the first/last angles and the quarter points.  Both
-angle-group plans (unaligned / ray-aligned, ADMM_FWD_PLAN) are checked.
+angle-group plans (64-ray chunks / aligned per segment and angle / aligned per segment and
+chunk, ADMM_FWD_PLAN) are checked.
 
 Tolerance (relative Frobenius over the checked rows): float32 samples 4e-6
 (sums of up to 2N float32 products per ray in 8 segment partials),
@@ -69,7 +70,7 @@ def _check(N, a, dtype, k, plan, seed):
 
 
 @pytest.mark.parametrize("N", [256, 512, 1024])
-@pytest.mark.parametrize("plan", [0, 1])
+@pytest.mark.parametrize("plan", [0, 1, 2])
 def test_grouped_forward_vb8_float32(cuda, N, plan):
     """8 images = the benchmark's k_fwdg<float, 8> instance (C2, C3/bench, C4 sizes)."""
     _check(N, 96, "float32", 8, plan, seed=N + plan)
@@ -81,7 +82,7 @@ def test_grouped_forward_narrow_batches(cuda, k):
     _check(512, 96, "float32", k, 1, seed=7 * k)
 
 
-@pytest.mark.parametrize("plan", [0, 1])
+@pytest.mark.parametrize("plan", [0, 1, 2])
 def test_grouped_forward_2048_float64(cuda, plan):
     """C5 size and precision: 2048^2, 96 angles per node, float64 samples, 8 images."""
     _check(2048, 96, "float64", 8, plan, seed=2048 + plan)
@@ -91,6 +92,7 @@ def test_grouped_forward_default_angles(cuda):
     """C1-style per-node angle counts (180 total over 4 nodes = 45: one angle at pi/2)."""
     _check(64, 45, "float32", 4, 1, seed=45)
     _check(64, 45, "float64", 4, 0, seed=46)
+    _check(64, 45, "float32", 4, 2, seed=47)
 
 
 def _check_adjoint(N, a, dtype, k, seed, tol):
@@ -121,3 +123,31 @@ def test_adjoint_1024_float32(cuda):
 def test_adjoint_2048_float64(cuda):
     """C5 size and precision: A^T at 2048^2, 96 angles, float64 samples."""
     _check_adjoint(2048, 96, "float64", 1, 12, 1e-12)
+
+
+def _bound_plans(N, dtype):
+    """The forward plans of an 8-node batch bound at N^2 (admm_fwd_plan_info)."""
+    import networkx as nx
+    from admm_hip.data import make_precisions, make_sinograms
+    from admm_hip.plan import make_plan
+    from admm_hip.solver import NodeBatch, make_operators
+    ops = make_operators(N, 8, angles_total=96 * 8, dtype=dtype, device=0)
+    plan = make_plan(nx.cycle_graph(8), 8, 1, 0)
+    ph = shepp_logan(N)
+    sinos = dict(zip(plan.local_nodes, make_sinograms(ops, ph, 0.005, seed=1)))
+    _, Q = make_precisions(ops)
+    nb = NodeBatch(ops[0].geom, dtype, plan, sinos, Q, 2.0, 0.02, 0.2, 10, 5, "iso", ph, 0)
+    return {p["plan"]: p for p in nb.fwd_plans()}
+
+
+def test_planner_picks_chunk_aligned_plan_for_large_images(cuda):
+    """At 2048^2 the per-(segment, angle) alignment lets 64-ray chunks far from the detector
+    centre drift apart (the rays' spacing differs between a group's angles), so its groups
+    shrink; the chunk-aligned plan stages half the row pixels in fewer blocks and is bound
+    (1141 vs 1439 us per float64 launch, profiles/r3_forward_plans.jsonl).  At 512^2 the
+    64-ray plan keeps two blocks per CU and stays bound."""
+    p = _bound_plans(2048, "float64")
+    assert p[2]["active"], p
+    assert p[2]["staged_px"] < 0.6 * p[1]["staged_px"] and p[2]["blocks"] < p[1]["blocks"], p
+    p = _bound_plans(512, "float32")
+    assert p[0]["active"] and p[0]["blocks"] == 512, p
