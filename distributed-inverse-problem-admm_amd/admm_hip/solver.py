@@ -150,7 +150,8 @@ class NodeBatch:
     def ctx_vb(self) -> int:
         """Node-interleave width the library uses for this batch (admm_tomo.hip vb_for)."""
         V = self.plan.V
-        return 8 if V >= 5 else 4 if V >= 3 else V
+        vb = 8 if V >= 5 else 4 if V >= 3 else V
+        return min(vb, 4) if self.dtype == "float64" else vb
 
     @property
     def x_local(self) -> torch.Tensor:

@@ -164,7 +164,13 @@ namespace {
 
 constexpr int kXcds = 8;  // MI355X: 8 XCDs, workgroups dealt round-robin (id % 8)
 
-int vb_for(int V) { return V >= 5 ? 8 : (V >= 3 ? 4 : (V == 2 ? 2 : 1)); }
+// Node-interleave width of a batch of V nodes: 32-byte sample vectors at most for float64
+// (8 float64 nodes = 64 B would need 4 sample planes per tap: the forward loses its
+// LDS-DMA staging, the back projector spills at 128 VGPRs; C5s 65.0 vs 63.0 node-updates/s)
+int vb_for(int V, int dtype) {
+  const int vb = V >= 5 ? 8 : (V >= 3 ? 4 : (V == 2 ? 2 : 1));
+  return dtype == ADMM_DTYPE_F64 ? std::min(vb, 4) : vb;
+}
 
 void select_fwd_plan(admm_ctx* C, int pl) {
   C->groups = C->plan_groups[pl];
@@ -649,7 +655,7 @@ int op_forward(admm_ctx* C, const T* img, T* sino, int nimg, hipStream_t s) {
     return launch_fwd<T, 1, 0>(C, img, (const T*)C->op_imgT.p, sino, nullptr, nullptr, nimg, s);
   }
   const int cmax = std::min(nimg, 8);
-  const int vbmax = vb_for(cmax);
+  const int vbmax = vb_for(cmax, C->dtype);
   RET(ensure(C->op_img, vbmax * npix * ds));
   RET(ensure(C->op_imgT, vbmax * npix * ds));
   RET(ensure(C->op_sino, vbmax * m * ds));
@@ -658,7 +664,7 @@ int op_forward(admm_ctx* C, const T* img, T* sino, int nimg, hipStream_t s) {
     const int nc = std::min(8, nimg - v0);
     const T* in = img + (size_t)v0 * npix;
     T* out = sino + (size_t)v0 * m;
-    RET(with_vb(vb_for(nc), [&](auto vbc) { return op_forward_chunk<T, decltype(vbc)::value>(C, in, out, nc, s); }));
+    RET(with_vb(vb_for(nc, C->dtype), [&](auto vbc) { return op_forward_chunk<T, decltype(vbc)::value>(C, in, out, nc, s); }));
   }
   return ADMM_OK;
 }
@@ -1013,11 +1019,13 @@ int admm_ctx_destroy(admm_ctx* C) {
   DeviceGuard _dg(C->device);
   (void)hipDeviceSynchronize();
   free_graphs(C);
-  Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->op_sino, &C->op_fpart, &C->op_order[0], &C->op_order[1], &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->bI, &C->fpart, &C->r, &C->c,
+  Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->op_sino, &C->op_fpart, &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->bI, &C->fpart, &C->r, &C->c,
                  &C->d2, &C->e2, &C->partH, &C->partS, &C->partD, &C->partE, &C->redH, &C->fg_order, &C->dsumS, &C->ats,
                  &C->f_ptr, &C->f_idx, &C->f_val, &C->t_ptr, &C->t_idx, &C->t_val, &C->x2, &C->p2, &C->pring};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
+  for (Buf& b : C->op_order)
+    if (b.p) (void)hipFree(b.p);
   if (C->fang) (void)hipFree(C->fang);
   if (C->bang) (void)hipFree(C->bang);
   if (C->bangc) (void)hipFree(C->bangc);
@@ -1116,7 +1124,7 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   RET(free_graphs(C));
   C->b = B;
   const int V = B.V;
-  C->vb = vb_for(V);
+  C->vb = vb_for(V, C->dtype);
   RET(with_vb(C->vb, [&](auto vbc) {
     constexpr int VB = decltype(vbc)::value;
     return C->dtype == ADMM_DTYPE_F32 ? choose_fwd_plan<float, VB>(C, V) : choose_fwd_plan<double, VB>(C, V);

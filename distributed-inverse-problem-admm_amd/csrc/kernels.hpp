@@ -1297,7 +1297,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
   // CU otherwise waits for every chunk's loads with nothing to overlap; +12 VGPRs, still
   // 4 waves/SIMD); kmin is double-buffered.  Otherwise: compute kmin, stage, tap per chunk.
   // (float samples, H/INIT modes: the float64 and DIAG variants would spill)
-  constexpr bool PF = std::is_same<T, float>::value && (MODE == BACK_H || MODE == BACK_INIT ||
+  constexpr bool PF = (std::is_same<T, float>::value || NPL <= 2) && (MODE == BACK_H || MODE == BACK_INIT ||
                                                                      MODE == BACK_PLAIN || MODE == BACK_ATB);
   constexpr int SPER = (ANGC * kBWin * NPL + kBkThreads - 1) / kBkThreads;
   Pack<T, PV> wst[SPER];
