@@ -654,14 +654,15 @@ int op_forward(admm_ctx* C, const T* img, T* sino, int nimg, hipStream_t s) {
     CHECK_LAUNCH();
     return launch_fwd<T, 1, 0>(C, img, (const T*)C->op_imgT.p, sino, nullptr, nullptr, nimg, s);
   }
-  const int cmax = std::min(nimg, 8);
+  const int step = vb_for(8, C->dtype);  // images per chunk: one sample vector (8 float32 / 4 float64)
+  const int cmax = std::min(nimg, step);
   const int vbmax = vb_for(cmax, C->dtype);
   RET(ensure(C->op_img, vbmax * npix * ds));
   RET(ensure(C->op_imgT, vbmax * npix * ds));
   RET(ensure(C->op_sino, vbmax * m * ds));
   RET(ensure(C->op_fpart, (size_t)kFgSeg * vbmax * m * ds));
-  for (int v0 = 0; v0 < nimg; v0 += 8) {
-    const int nc = std::min(8, nimg - v0);
+  for (int v0 = 0; v0 < nimg; v0 += step) {
+    const int nc = std::min(step, nimg - v0);
     const T* in = img + (size_t)v0 * npix;
     T* out = sino + (size_t)v0 * m;
     RET(with_vb(vb_for(nc, C->dtype), [&](auto vbc) { return op_forward_chunk<T, decltype(vbc)::value>(C, in, out, nc, s); }));
