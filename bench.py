@@ -140,8 +140,9 @@ def _cpu_worker(wid, N, a, b, q, budget, barrier, out):
         D = 2 * q
         delta, gap, rn, eps = eq1.certificate(A, b, D, 2 * q * v, st0.x, prm.mu * st0.ex / prm.lam,
                                               prm.mu * st0.ey / prm.lam, N, prm.rho, prm.lam, "iso")
+        f = ons.objective(A, b, st0.x, N, prm.rho, prm.lam, [(q, v), (q, v)], "iso")  # eq.(1) at x
         cert = dict(dist_bound=delta, rel_dist_bound=delta / float(np.linalg.norm(st0.x)), obj_gap_bound=gap,
-                    stationarity=rn, eps=eps, m=float(prm.rho * D.min()))
+                    objective=f, rel_obj_gap_bound=gap / f, stationarity=rn, eps=eps, m=float(prm.rho * D.min()))
     out.put((wid, done, el, x if wid == 0 else None, cert))
 
 
@@ -189,7 +190,8 @@ def cpu_baseline(N, a, b, q, x_gpu, procs=None, budget=CPU_BASELINE_SECONDS):
                                        "GPU matches to rel_fro) from eq.(1)'s exact minimiser "
                                        "(block_5_node_problem.py:21-29): split-Bregman dual p = mu e / lam, "
                                        "strong convexity m = rho min(D) (a lower bound on lambda_min(H)); "
-                                       "obj_gap_bound = ||r||^2 / 2m + eps >= f(x) - f(x*); the reference's "
+                                       "obj_gap_bound = ||r||^2 / 2m + eps >= f(x) - f(x*), objective = f(x) (eq.(1)), "
+                                       "rel_obj_gap_bound = obj_gap_bound / f(x); the reference's "
                                        "SCS solve is inexact too (eps = min(1e-2, eps_target))"),
             "sample": f"{done} x-updates of node 0's first ADMM iteration ({N}^2, {a} angles, 2 ring "
                       f"neighbours, 10x5 inner, zero start) on the GPU run's own float32 sinogram "
@@ -429,6 +431,9 @@ def main():
     roof = {
         "kernel": f"k_fwdg<{'double' if dtype == 'float64' else 'float'},{nb.ctx_vb}> (Joseph forward "
                   "projector taps, angle-grouped, 8 row-segment partial sums per ray)",
+        # the angle-group plan the batch bound (admm_fwd_plan_info): 0 = 64-ray chunks,
+        # 1 = aligned per (segment, angle), 2 = aligned per (segment, chunk)
+        "fwd_plan": next((dict(p) for p in nb.fwd_plans() if p["active"]), None),
         "bound": "hbm",
         "achieved": fwd_traffic / fwd_s / 1e9 if fwd_traffic is not None else None,
         "peak": HBM_PEAK_GBS,

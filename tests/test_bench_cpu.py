@@ -50,6 +50,9 @@ def test_cpu_baseline_reports_eq1_certificate():
     c = r["eq1_gap"]
     assert c["m"] > 0 and c["dist_bound"] > 0 and c["obj_gap_bound"] >= c["eps"] >= 0
     assert c["dist_bound"] >= c["stationarity"] / c["m"]
+    # eq.(1)'s objective at the oracle image and the gap bound relative to it
+    assert c["objective"] > c["obj_gap_bound"] > 0
+    assert abs(c["rel_obj_gap_bound"] - c["obj_gap_bound"] / c["objective"]) < 1e-15
 
 
 def test_c4_graph_matches_committed_adjacency():
