@@ -68,11 +68,30 @@ class ShardPlan:
         return len(self.local_nodes) + len(self.halo_nodes)
 
     def use_allgather(self) -> bool:
-        """All-gather when a rank needs most remote images (dense / ER graphs)."""
+        """All-gather when some rank needs most of its remote images (dense / ER graphs).
+
+        The exchange is a collective, so the choice is made from the whole graph and node
+        partition -- the same on every rank (a rank-local choice let C4's 32-node ER graph
+        on 8 ranks put one rank in p2p mode while the others all-gathered: a deadlock)."""
         if self.world == 1:
             return False
-        remote = self.V_total - self.V
-        return remote > 0 and len(self.halo_nodes) * 2 > remote
+        cached = self.__dict__.get("_allgather")
+        if cached is None:
+            owner = np.empty(self.V_total, dtype=np.int64)
+            for r, (lo, hi) in enumerate(self.ranges):
+                owner[lo:hi] = r
+            halo = [set() for _ in range(self.world)]
+            for a, b in self.edges:
+                ra, rb = int(owner[a]), int(owner[b])
+                if ra != rb:
+                    halo[ra].add(b)
+                    halo[rb].add(a)
+            cached = False
+            for r, (lo, hi) in enumerate(self.ranges):
+                remote = self.V_total - (hi - lo)
+                cached = cached or (remote > 0 and len(halo[r]) * 2 > remote)
+            self.__dict__["_allgather"] = cached
+        return cached
 
 
 def canonical_edges(G, V_total: int) -> list:

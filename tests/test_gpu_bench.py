@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _run(*args, env=None):
     out = subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, capture_output=True, text=True,
-                         timeout=300, check=True, env=env).stdout
+                         timeout=540, check=True, env=env).stdout
     lines = [l for l in out.splitlines() if l.strip().startswith("{")]
     assert len(lines) == 1, out
     return json.loads(lines[0])
@@ -48,6 +48,19 @@ def test_bench_launches_its_own_ranks(cuda):
     b = _run("--gpus", "2", "--steps", "2", "--warmup", "1", "--strong", "none", env=env)
     assert b["n_gpus"] == 2 and b["config"]["nodes"] == 16
     assert b["exchange_check"]["ok"] and b["exchange_check"]["halo_rows"] == 4
+
+
+@pytest.mark.timeout(600)
+def test_bench_eight_ranks_with_strong_c4(cuda):
+    """The driver's N = 8 command shape (``bench.py --gpus 8``, default strong leg C4) as a
+    gloo rehearsal on this one GPU: 64-node ring over 8 self-launched ranks, then C4's
+    32-node ER graph over the same 8 ranks (all-gather exchange on every rank)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["ADMM_DIST_BACKEND"] = "gloo"
+    b = _run("--gpus", "8", "--steps", "1", "--warmup", "1", "--strong-steps", "1", env=env)
+    assert b["n_gpus"] == 8 and b["config"]["nodes"] == 64
+    assert b["exchange_check"]["ok"] and b["exchange_check"]["mode"] == "p2p"
+    assert b["strong"]["config"] == "C4" and b["strong"]["value"] > 0
 
 
 def test_bench_config_line(cuda):

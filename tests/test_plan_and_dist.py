@@ -28,6 +28,34 @@ def graphs():
     yield "er9", nx.erdos_renyi_graph(9, 0.35, seed=seed)
 
 
+def scale_graphs():
+    """The graphs the 8-GPU runs use: the bench's default workload at N = 8 (a ring of 64),
+    C4's 32-node Erdos-Renyi graph (committed fixture) and C5's 64-node complete graph."""
+    import json
+    yield "ring64", nx.cycle_graph(64)
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c4_er32_graph.json")) as f:
+        fx = json.load(f)
+    G = nx.Graph()
+    G.add_nodes_from(range(fx["nodes"]))
+    G.add_edges_from(map(tuple, fx["edges"]))
+    yield "er32", G
+    yield "complete64", nx.complete_graph(64)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_exchange_mode_is_the_same_on_every_rank(world):
+    """HaloExchange is a collective: p2p or all-gather must be one global choice.  C4's
+    ER graph on 8 ranks has ranks on both sides of the per-rank density threshold."""
+    for name, G in list(graphs()) + list(scale_graphs()):
+        V = G.number_of_nodes()
+        if V < world:
+            continue
+        modes = {make_plan(G, V, world, r).use_allgather() for r in range(world)}
+        assert len(modes) == 1, (name, world)
+    G = dict(scale_graphs())["er32"]
+    assert make_plan(G, 32, 8, 0).use_allgather()
+
+
 @pytest.mark.parametrize("world", [1, 2, 3, 4])
 def test_plan_partitions_nodes_and_edges(world):
     for name, G in graphs():
@@ -281,7 +309,7 @@ def _halo_check_rank(rank, world, port, gname, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from admm_hip.exchange import HaloExchange, verify_halo
-        G = dict(graphs())[gname]
+        G = dict(list(graphs()) + list(scale_graphs()))[gname]
         V = G.number_of_nodes()
         plan = make_plan(G, V, world, rank)
         n = 37
@@ -299,7 +327,8 @@ def _halo_check_rank(rank, world, port, gname, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("gname,world", [("ring8", 2), ("complete6", 2), ("ring8", 4)])
+@pytest.mark.parametrize("gname,world", [("ring8", 2), ("complete6", 2), ("ring8", 4), ("ring64", 8),
+                                         ("er32", 8), ("complete64", 8)])
 def test_verify_halo_detects_exchange_errors(gname, world):
     """bench.py's N > 1 exchange check (admm_hip.exchange.verify_halo): after HaloExchange.run
     every halo row equals its owner's row byte for byte; before it, or with one bit
