@@ -448,14 +448,14 @@ __global__ __launch_bounds__(kBlock) void k_csr_fwd(const int* __restrict__ ptr,
 
 // ===========================================================================
 // Forward projector, angle-grouped (the hot-path version).
-// Block = G <= 4 consecutive angles of one case (one wave each) x 64 consecutive
-// detector bins, over one of kFgSeg row segments.  Rows are processed in chunks of
-// kFgRows: for each row the block stages into LDS the window of image pixels
-// (columns wlo .. wlo+kFgWin-1) that any of its G x 64 rays can touch, zero-filled
-// outside the image, then every ray takes its two taps per row from LDS.  One
-// staged pixel serves ~G x 1.4 x 2 taps, so texture-path traffic drops ~G-fold
-// and taps run at LDS rate.  The host sizes groups so the window fits
-// (FgGroup tables; wider N -> smaller G).  Segment partial sums go to
+// Block = G <= kFgG consecutive angles of one case (one wave each) x up to 64 rays of
+// each (its FgRange entry), over one of kFgSeg row segments.  Rows are processed in
+// chunks (2 rows, LDS-DMA double buffer): for each row the block stages into LDS the
+// window of image pixels (columns wlo .. wlo+kFgWin-1) that any of its rays can touch,
+// zero-filled outside the image, then every ray takes its two taps per row from LDS.
+// One staged pixel serves ~G x 1.4 x 2 taps, so L2 traffic drops ~G-fold and taps run
+// at LDS rate.  The host plans groups and per-block ray ranges so every window fits
+// (FgGroup / FgRange tables, three plans; admm_tomo.hip).  Segment partial sums go to
 // part[seg][chunk][ray][VB] and k_fwd_combine adds them in fixed order.
 //
 // LDS bank conflicts.  Adjacent rays sit A1 in [1, 1.41] pixels apart, so a
