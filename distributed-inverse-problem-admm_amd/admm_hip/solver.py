@@ -209,10 +209,10 @@ class NodeBatch:
 
     def fwd_plans(self) -> list[dict]:
         """The grouped forward projector's plans for this batch's geometry (admm_fwd_plan_info):
-        per plan 0/1/2 its angle groups, blocks per node chunk, staged row pixels (host model)
+        per plan 0-5 its angle groups, blocks per node chunk, staged row pixels (host model)
         and whether it is the bound one; plans the geometry does not have are omitted."""
         out = []
-        for pl in range(3):
+        for pl in range(6):
             g, b, a, st = C.c_int(), C.c_int(), C.c_int(), C.c_double()
             _lib.check(self.lib.admm_fwd_plan_info(self.ctx.h, pl, C.byref(g), C.byref(b), C.byref(st),
                                                    C.byref(a)), "admm_fwd_plan_info")

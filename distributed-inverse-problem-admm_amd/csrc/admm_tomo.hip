@@ -107,9 +107,11 @@ struct admm_ctx {
   FgGroup* groups = nullptr;  // angle groups of the grouped forward projector (active plan)
   FgRange* rng = nullptr;     // its per-block ray ranges
   int n_groups = 0;           // 0: geometry does not fit the grouped kernel -> k_fwd
-  // the group plans (0: 64-ray chunks, 1: chunks aligned per (row segment, angle) at the
-  // detector centre, 2: chunks aligned per (row segment, chunk)), chosen at bind time
-  static constexpr int kPlans = 3;
+  // the group plans, chosen at bind time: 0: 64-ray chunks, 1: chunks aligned per (row
+  // segment, angle) at the detector centre, 2: chunks aligned per (row segment, chunk);
+  // 3-5: the same with every block's rays clipped to those crossing its segment inside the
+  // image (groups re-planned on the narrower windows)
+  static constexpr int kPlans = 6;
   FgGroup* plan_groups[kPlans] = {};
   FgRange* plan_rng[kPlans] = {};
   int plan_n[kPlans] = {}, plan_blocks[kPlans] = {};
@@ -130,6 +132,7 @@ struct admm_ctx {
   Buf op_img, op_imgT, op_sino, op_fpart;
   Buf op_order[kPlans];  // block tables of the forward plans for one node chunk
   int op_nblk[kPlans] = {};
+  int op_fpart_key = -1;  // (plan, VB) whose partial slots op_fpart holds (others are zero)
 
   // batch
   bool bound = false;
@@ -238,9 +241,12 @@ int build_fwd_order(admm_ctx* C, int pl, int nch, int cus) {
 // Forward plan for the bound batch: the ray-aligned plan stages less per tap but has one
 // more chunk per (group, segment); take it unless the busiest CU would host more of its
 // blocks (e.g. 512^2: 512 unaligned blocks put 2 on every one of 256 CUs, the aligned 528
-// put 3 on some; co-resident blocks share the CU).  The chunk-aligned plan (2) replaces it
-// when it stages fewer pixels without more blocks per CU (large images: 2048^2 stages half
-// the pixels of plan 1 in 2/3 of its blocks).  ADMM_FWD_PLAN=0/1/2 forces a plan.
+// put 3 on some; co-resident blocks share the CU).  When that plan needs more than one round
+// of blocks, the plan staging the fewest pixels replaces it (1024^2, 2048^2: the chunk-
+// aligned plan with clipped rays, 107 / 870 us against 130 / 1020 for the best unclipped
+// one); in one round the 64-ray plan's equal segment shares keep every XCD on its own
+// row band (512^2: 31.2 us; the clipped plans' 440-492 blocks run 35.5-37).
+// ADMM_FWD_PLAN=0..5 forces a plan.
 // (The occupancy query only guards against a plan that cannot be resident at all.)
 template <typename T, int VB>
 int pick_fwd_plan(admm_ctx* C, int nch, int* pl_out, int* cus_out) {
@@ -250,9 +256,14 @@ int pick_fwd_plan(admm_ctx* C, int nch, int* pl_out, int* cus_out) {
   if (per_cu < 1) return fail(ADMM_E_HIP, "grouped forward projector cannot be resident");
   auto per_cu_max = [&](int pl) { return ((long)C->plan_blocks[pl] * nch + cus - 1) / std::max(1, cus); };
   int pl = per_cu_max(1) <= per_cu_max(0) ? 1 : 0;
-  if (C->plan_n[2] > 0 && per_cu_max(2) <= per_cu_max(pl) && C->plan_staged[2] < C->plan_staged[pl]) pl = 2;
+  if (per_cu_max(pl) > per_cu) {
+    // more than one round of blocks: the plan staging the fewest row pixels (large images,
+    // where staging from beyond L2 and the rays missing a segment dominate)
+    for (int q = 0; q < admm_ctx::kPlans; ++q)
+      if (C->plan_n[q] > 0 && C->plan_staged[q] < C->plan_staged[pl]) pl = q;
+  }
   const char* f = getenv("ADMM_FWD_PLAN");
-  if (f && f[0] >= '0' && f[0] <= '2' && C->plan_n[f[0] - '0'] > 0) pl = f[0] - '0';
+  if (f && f[0] >= '0' && f[0] < '0' + admm_ctx::kPlans && C->plan_n[f[0] - '0'] > 0) pl = f[0] - '0';
   *pl_out = pl;
   *cus_out = cus;
   return ADMM_OK;
@@ -625,6 +636,10 @@ int op_forward_chunk(admm_ctx* C, const T* img, T* sino, int nc, hipStream_t s) 
   int pl = 0, cus = 0;
   RET((pick_fwd_plan<T, VB>(C, 1, &pl, &cus)));
   if (C->op_nblk[pl] == 0) RET(build_fwd_order_into(C, pl, 1, cus, C->op_order[pl], &C->op_nblk[pl]));
+  if (C->op_fpart_key != pl * 16 + VB) {  // slots another plan / width wrote: back to 0
+    HIPCHK(hipMemsetAsync(C->op_fpart.p, 0, C->op_fpart.bytes, s));
+    C->op_fpart_key = pl * 16 + VB;
+  }
   T* xs = (T*)C->op_img.p;
   T* xsT = (T*)C->op_imgT.p;
   T* sI = (T*)C->op_sino.p;
@@ -787,6 +802,8 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
                           std::vector<int4>& bv, double& st) -> bool {
       for (int q = 0; q < G; ++q)
         if (fa[t0 + q].caseA != fa[t0].caseA) return false;
+      const int scheme = pl % 3;
+      const bool clipped = pl >= 3;
       gr = FgGroup{};
       gr.t0 = t0;
       gr.G = G;
@@ -796,7 +813,25 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
       for (int s = 0; s < kFgSeg; ++s) {
         const int mlo = s * g.N / kFgSeg, mhi = (s + 1) * g.N / kFgSeg;
         const double mc = 0.5 * (mlo + mhi - 1);
-        auto emit = [&](const FgRange& r) -> bool {
+        // only rays that cross the segment's rows inside the image get lanes: a ray whose every
+        // row position l lies outside [-2, N + 1] taps zero-filled columns only, so its partial
+        // for this segment is exactly 0 and its slot keeps the zero it was filled with
+        // (admm_batch_bind / op_forward_chunk zero the partials when the plan changes)
+        const double dlo = std::min(mlo * 1.0, mhi - 1.0), dhi = std::max(mlo * 1.0, mhi - 1.0);
+        auto clip = [&](FgRange& r) {
+          for (int q = 0; q < G; ++q) {
+            const FwdAngle& b = fa[t0 + q];
+            const double e0 = std::min(dlo * b.dl, dhi * b.dl), e1 = std::max(dlo * b.dl, dhi * b.dl);
+            const double ka = (-2.0 - b.A0 - e1) / b.A1, kb = (g.N + 1.0 - b.A0 - e0) / b.A1;
+            const double klo = std::ceil(std::min(ka, kb)), khi = std::floor(std::max(ka, kb));
+            const int lo = (int)std::max((double)r.k0[q], klo);
+            const int hi = (int)std::min((double)(r.k0[q] + r.nk[q]), khi + 1.0);
+            r.nk[q] = std::max(0, hi - lo);
+            r.k0[q] = std::min(std::max(lo, 0), g.n_det - 1);
+          }
+        };
+        auto emit = [&](FgRange r) -> bool {
+          if (clipped) clip(r);
           bool any = false;
           for (int q = 0; q < G; ++q) any = any || r.nk[q] > 0;
           if (!any) return true;
@@ -807,13 +842,13 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
           rv.push_back(r);
           return true;
         };
-        if (pl < 2) {
+        if (scheme < 2) {
           const FwdAngle& r0 = fa[t0];
           const double lref = r0.A0 + cd * r0.A1 + mc * r0.dl;  // reference ray at the centre row
           int dmin = 0, dmax = 0;
           for (int q = 0; q < G; ++q) {
             const FwdAngle& b = fa[t0 + q];
-            const int d = pl == 1 ? (int)std::lround((lref - b.A0 - cd * b.A1 - mc * b.dl) / b.A1) : 0;
+            const int d = scheme == 1 ? (int)std::lround((lref - b.A0 - cd * b.A1 - mc * b.dl) / b.A1) : 0;
             gr.delta[s][q] = d;
             dmin = std::min(dmin, d);
             dmax = std::max(dmax, d);
@@ -884,7 +919,7 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
         while (G > 1 && !plan_group(t0, G, pl, gi, gr, rv, bv, st)) --G;
         if (G == 1 && !plan_group(t0, 1, pl, gi, gr, rv, bv, st)) {
           if (pl < 2) fits = false;  // no grouped kernel for this geometry
-          groups_plan[pl].clear();   // (plan 2 is optional)
+          groups_plan[pl].clear();   // (plans 2-5 are optional)
           break;
         }
         const int base = (int)rng_plan[pl].size();
@@ -1146,7 +1181,13 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   C->ats_valid = false;
   RET(ensure(C->sino, Vp * m * ds));
   RET(ensure(C->bI, Vp * m * ds));
-  if (C->n_groups > 0) RET(ensure(C->fpart, (size_t)kFgSeg * Vp * m * ds));
+  if (C->n_groups > 0) {
+    RET(ensure(C->fpart, (size_t)kFgSeg * Vp * m * ds));
+    // the plan writes only the (segment, ray) partials of rays crossing the segment inside
+    // the image; every other slot must read as 0 in k_fwd_combine
+    HIPCHK(hipMemset(C->fpart.p, 0, C->fpart.bytes));
+    HIPCHK(hipDeviceSynchronize());
+  }
   RET(ensure(C->r, V * npix * 8));
   RET(ensure(C->c, V * npix * 8));
   RET(ensure(C->d2, 2 * V * npix * 8));

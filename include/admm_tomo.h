@@ -208,7 +208,8 @@ int admm_consensus(admm_ctx* ctx, void* stream);
 int admm_time_forward(admm_ctx* ctx, int reps, int in_solve, void* stream, double* ms_out);
 /* ABI 6: the grouped forward projector's plan `plan` (0: 64-ray chunks, 1: chunks aligned
  * per (row segment, angle) at the detector centre, 2: chunks aligned per (row segment,
- * chunk)) for this context's geometry: angle groups, blocks per node chunk, touched row
+ * chunk); 3-5: plans 0-2 with each block's rays clipped to those crossing its row segment
+ * inside the image) for this context's geometry: angle groups, blocks per node chunk, touched row
  * pixels staged per node chunk (the host planner's model), and active = 1 if it is the plan
  * the bound batch (or, before a bind, the context) uses.  groups = 0: no such plan.
  * No device work.  (Tests and tuning; the plans give bitwise-identical projections.) */

@@ -2,7 +2,7 @@
 
 For each image size (env SIZES, default "512:float32,1024:float32,2048:float64") and each
 plan the geometry has (0: 64-ray chunks, 1: aligned per (segment, angle), 2: aligned per
-(segment, chunk)), binds an 8-node batch with ADMM_FWD_PLAN forcing the plan and prints the
+(segment, chunk); 3-5: the same with rays clipped to each segment), binds an 8-node batch with ADMM_FWD_PLAN forcing the plan and prints the
 planner's groups / blocks / staged pixels with the average tap-launch time back to back and
 in-solve (one x-update's 50 CG-step forwards), one JSON line per (size, plan)."""
 import json
@@ -27,7 +27,7 @@ for item in os.environ.get("SIZES", "512:float32,1024:float32,2048:float64").spl
     ph = shepp_logan(N)
     sinos = dict(zip(plan.local_nodes, make_sinograms(ops, ph, 0.005, seed=1000)))
     Wi, Q = make_precisions(ops)
-    for pl in (0, 1, 2):
+    for pl in range(6):
         os.environ["ADMM_FWD_PLAN"] = str(pl)
         nb = NodeBatch(ops[0].geom, dt, plan, sinos, Q, 2.0, 0.02, 0.2, 10, 5, "iso", ph, 0, keep_x=True)
         info = {p["plan"]: p for p in nb.fwd_plans()}

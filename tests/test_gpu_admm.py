@@ -170,13 +170,15 @@ def test_deterministic_bitwise(cuda):
 @pytest.mark.parametrize("N,V,angles,dtype", [(96, 8, 384, "float32"), (64, 5, 200, "float64")])
 def test_forward_plans_bitwise_equal(cuda, monkeypatch, N, V, angles, dtype):
     """The grouped forward projector's ray layouts (plain 64-ray chunks, rays aligned per
-    row segment and angle, chunks aligned per row segment and chunk) and block orders only
+    row segment and angle, chunks aligned per row segment and chunk, each with and without
+    rays clipped to the segment -- a clipped ray's partial is an exact 0) and block orders only
     redistribute work: every (segment, ray) partial is
     the same sum in the same order, so whole ADMM runs are bitwise identical."""
     ops, ph, sinos, Wi, Q, A, _ = setup_problem(N, V, angles, dtype)
     G = nx.cycle_graph(V)
     runs = []
-    for plan, natural in (("0", "0"), ("1", "0"), ("2", "0"), ("0", "1"), ("1", "1"), ("2", "1")):
+    for plan, natural in (("0", "0"), ("1", "0"), ("2", "0"), ("3", "0"), ("4", "0"), ("5", "0"),
+                          ("0", "1"), ("2", "1"), ("5", "1")):
         monkeypatch.setenv("ADMM_FWD_PLAN", plan)
         monkeypatch.setenv("ADMM_FWD_NATURAL_ORDER", natural)
         runs.append(decentralized_admm(ops, sinos, G, Wi, Q, N, lam_tv=0.02, rho=2.0, max_iters=2,

@@ -126,7 +126,7 @@ def test_large_x_updates_match_operator_oracle(cuda, monkeypatch, N, V, dtype, t
     ops, ph, sinos, Wi, Q = problem(N, V, 96, dtype)
     G = nx.cycle_graph(V) if graph == "ring" else nx.complete_graph(V)
     runs = []
-    for plan in ("0", "1", "2"):
+    for plan in ("0", "1", "2", "5"):
         monkeypatch.setenv("ADMM_FWD_PLAN", plan)
         runs.append(gpu_run(ops, sinos, G, Wi, Q, N, 2, ph, tv_kind=tv, tv_iters=tvi))
     monkeypatch.delenv("ADMM_FWD_PLAN")
