@@ -845,23 +845,22 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
         if (scheme < 2) {
           const FwdAngle& r0 = fa[t0];
           const double lref = r0.A0 + cd * r0.A1 + mc * r0.dl;  // reference ray at the centre row
+          int delta[kFgG] = {};  // per-angle ray offset of the 64-ray chunks (scheme 1)
           int dmin = 0, dmax = 0;
           for (int q = 0; q < G; ++q) {
             const FwdAngle& b = fa[t0 + q];
             const int d = scheme == 1 ? (int)std::lround((lref - b.A0 - cd * b.A1 - mc * b.dl) / b.A1) : 0;
-            gr.delta[s][q] = d;
+            delta[q] = d;
             dmin = std::min(dmin, d);
             dmax = std::max(dmax, d);
           }
           const int kcb = (int)std::floor(-dmax / 64.0);
           const int kce = (int)std::ceil((g.n_det - dmin) / 64.0);
-          gr.kcb[s] = kcb;
-          gr.nkc[s] = kce - kcb;
           for (int kc = kcb; kc < kce; ++kc) {
             FgRange r{};
             for (int q = 0; q < G; ++q) {
-              const int lo = std::max(kc * 64 + gr.delta[s][q], 0);
-              const int hi = std::min(kc * 64 + gr.delta[s][q] + 64, g.n_det);
+              const int lo = std::max(kc * 64 + delta[q], 0);
+              const int hi = std::min(kc * 64 + delta[q] + 64, g.n_det);
               r.k0[q] = lo;
               r.nk[q] = std::max(0, hi - lo);
             }

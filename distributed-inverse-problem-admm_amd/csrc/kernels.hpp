@@ -500,24 +500,19 @@ __device__ __forceinline__ int fg_ray_of_lane(int lane) {
   return (lane & 32) + r;
 }
 
-// One angle group of the grouped forward projector.  Within row segment s, angle t0+q's
-// rays are shifted by delta[s][q] so that every angle of the group crosses the same
-// pixels at the segment's centre row (the union row window then spans the 64 rays plus
-// the angular spread over half a segment, not over half the image); block x of segment s
-// covers rays (kcb[s] + x) * 64 + delta[s][q] + [0, 64) of angle t0+q.
+// One angle group of the grouped forward projector: angles t0 .. t0+G-1 (one case).
 struct FgGroup {
   int t0, G;
-  int kcb[kFgSeg];          // first 64-ray chunk of each row segment (may be negative)
-  int nkc[kFgSeg];          // chunks of each row segment
-  int delta[kFgSeg][kFgG];  // per-angle ray offsets
 };
 // The rays one block projects: angle t0+q of its group takes rays k0[q] .. k0[q]+nk[q]-1
 // (0 <= nk <= 64, inside [0, n_det)).  Every plan is a table of these (one per (group,
-// segment, chunk)); per (group, segment) the ranges of each angle partition its rays.  The
-// fixed-chunk plans give every angle rays (kcb+x)*64 + delta + [0, 64) clipped to the
-// detector; the chunk-aligned plan starts every angle's chunk x at the same pixel of the
-// segment's centre row (a chunk spans 64 rays of the group's densest angle, so sparser
-// angles use fewer lanes), which keeps the union window narrow far from the detector centre.
+// segment, chunk)); per (group, segment) the ranges of each angle partition its rays (less
+// any ray a clipped plan drops because it misses the segment inside the image).  The
+// 64-ray plans give angle q rays x*64 + delta_q + [0, 64), delta_q = 0 or the shift that
+// makes every angle of the group cross the same pixels at the segment's centre row; the
+// chunk-aligned plan starts every angle's chunk x at the same pixel of that row (a chunk
+// spans 64 rays of the group's densest angle, so sparser angles use fewer lanes), which
+// keeps the union window narrow far from the detector centre too.
 struct FgRange {
   int k0[kFgG];
   int nk[kFgG];
