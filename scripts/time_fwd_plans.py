@@ -2,8 +2,8 @@
 
 For each image size (env SIZES, default "512:float32,1024:float32,2048:float64") and each
 plan the geometry has (0: 64-ray chunks, 1: aligned per (segment, angle), 2: aligned per
-(segment, chunk); 3-5: the same with rays clipped to each segment), binds an 8-node batch with ADMM_FWD_PLAN forcing the plan and prints the
-planner's groups / blocks / staged pixels with the average tap-launch time back to back and
+(segment, chunk); 3-5: the same with rays clipped to each segment), binds an 8-node batch
+with ADMM_FWD_PLAN forcing the plan and prints the planner's groups / blocks / staged pixels with the average tap-launch time back to back and
 in-solve (one x-update's 50 CG-step forwards), one JSON line per (size, plan)."""
 import json
 import os

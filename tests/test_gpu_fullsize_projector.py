@@ -7,7 +7,7 @@ matrix of oracle/geometry.py restricted to a handful of angles per case (the
 full matrix is ~2.4 GB at 1024^2 and ~10 GB at 2048^2): both sides of the
 45-degree case switch, the first/last angles and the quarter points.  Both
 angle-group plans (64-ray chunks / aligned per segment and angle / aligned per segment and
-chunk, ADMM_FWD_PLAN) are checked.
+chunk, each with and without rays clipped to the segment; ADMM_FWD_PLAN 0-5) are checked.
 
 Tolerance (relative Frobenius over the checked rows): float32 samples 4e-6
 (sums of up to 2N float32 products per ray in 8 segment partials),
