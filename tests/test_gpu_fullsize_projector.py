@@ -5,7 +5,7 @@ projector (admm_project_fwd packs the images into the node-interleaved sample
 layout, VB = 1/2/4/8 by image count).  The oracle is the float64 Joseph CSR
 matrix of oracle/geometry.py restricted to a handful of angles per case (the
 full matrix is ~2.4 GB at 1024^2 and ~10 GB at 2048^2): both sides of the
-45-degree case switch, the first/last angles and the quarter points.  Both
+45-degree case switch, the first/last angles and the quarter points.  All
 angle-group plans (64-ray chunks / aligned per segment and angle / aligned per segment and
 chunk, each with and without rays clipped to the segment; ADMM_FWD_PLAN 0-5) are checked.
 
