@@ -1,38 +1,55 @@
 """Benchmark: decentralized-ADMM node-updates/s on MI355X (BASELINE.json metric).
 
-Workload (weak scaling, one process per GPU): 512^2 modified Shepp-Logan,
-8 graph nodes per GPU with 96 angles each (N GPUs -> 8N-node ring; N=2 is
-BASELINE configs[2] exactly: 16 nodes, 1536 angles = 3N), lambda_TV = 0.02,
-rho = 2, split-Bregman 10 rounds x 5 CG steps per x-update, float32 projector
-samples / float64 solver state.  A "step" is one outer ADMM iteration: the
-x-update of every node, the halo exchange (RCCL), the z/y edge updates and the
-residual/statistics readback the reference's stop test needs (asynchronous, into pinned
-host memory: run_admm's pipelined mode).
+Headline workload (``--workload auto``):
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--strong C4|none]
+* one GPU: BASELINE.json configs[2] itself -- C3: 512^2 modified Shepp-Logan, a 16-node
+  ring, 96 angles per node (1536 = 3N in total), float32 projector samples / float64
+  solver state, lambda_TV = 0.02, rho = 2, split-Bregman 10 rounds x 5 CG steps per
+  x-update;
+* N > 1 GPUs (weak scaling, one process per GPU): the same per-node problem with 8 graph
+  nodes per GPU on a ring of 8N (N = 2 is C3 sharded over 2 GPUs exactly, as configs[2]
+  specifies).  The line also carries ``weak8`` at one GPU (8 nodes, the per-GPU share of
+  the N > 1 runs) and the strong-scaling legs ``strong`` (C3 and C4 -- 1024^2, 32-node
+  Erdos-Renyi graph -- sharded over the same N ranks; at one GPU only C4, C3 being the
+  headline).
+
+A "step" is one outer ADMM iteration: the x-update of every node, the halo exchange
+(RCCL), the z/y edge updates and the residual/statistics readback the reference's stop
+test needs (asynchronous, into pinned host memory: run_admm's pipelined mode, DESIGN.md
+section 9).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--strong C3,C4|none] [--proxy fast|all|none]
     torchrun --nproc-per-node N bench.py --gpus N ...
-    python bench.py --config C2|C3|C4|C5|C5s   (BASELINE.json configs[1..4], fixed node count,
-                                                 sharded over however many ranks run it)
+    python bench.py --config C2|C3|C4|C5|C5s [--as-rank R/W]
 
 ``python bench.py --gpus N`` with N > 1 and no WORLD_SIZE in the environment launches
 the N ranks itself (one child process per GPU, RANK / LOCAL_RANK / WORLD_SIZE /
 MASTER_ADDR=127.0.0.1 / MASTER_PORT set; the parent makes no GPU call), relays rank 0's
 line and exits non-zero if any rank fails.  Under a launcher, --gpus must equal WORLD_SIZE.
 
-Rank 0 prints one JSON line.  Besides the weak-scaling headline, the line carries a
-strong-scaling measurement (``strong``: BASELINE configs[3], C4 = 1024^2 / 32-node
-Erdos-Renyi graph, fixed total work, sharded over the same N ranks), so one driver
-sweep over N yields both curves.
+Per-rank proxies (``proxy_8gpu``, one GPU only).  The multi-GPU runs shard graph nodes,
+and every rank's x-updates are independent within an iteration
+(block_6_admm_loop_ver2.py:81-97), so rank R of a W-rank run does exactly its own share:
+its contiguous node block (one device batch at its own node-interleave width, e.g. 4
+nodes at VB = 4 for C4 on 8 GPUs), every halo row and every stored edge of
+plan.make_plan(G, V, W, R).  A proxy binds that share on this one GPU and times
+x-update + consensus + statistics with the halo rows held fixed; the exchange is
+priced from its bytes over xGMI (7 links x 153 GB/s per MI355X, task spec): ``direct``
+spreads the received bytes over min(peers, 7) links, ``one_link`` puts them on one.
+predicted_speedup = T_1 / (T_rank + t_exchange), T_1 = the config on one GPU (measured
+in the same run); ``per_node_cost_ratio`` = (T_rank / V_rank) / (T_1 / V).  ``--as-rank
+R/W`` with ``--config`` prints one such share as its own line.
 
 Roofline (``roofline``): the dominant kernel is the forward projector's tap kernel
 k_fwdg.  Its average launch duration is measured live with HIP events on the stream it
 runs on; its HBM bytes per launch come from the committed rocprofv3 PMC passes
-(2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md) of the in-solve launches
-(TRAFFIC_FILE), so ``frac`` = PMC bytes / live duration / 8 TB/s.  ``compulsory_bytes``
-is what one launch must move at least (each node image read once, its sinogram written
-once); ``sample_touch`` is SURVEY.md 8d's per-tap accounting, which counts LDS-served
-taps and so exceeds any memory peak -- it is reported as a reuse factor, not a rate.
-``step_hbm`` is the whole step's PMC traffic over the measured step time.
+(2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md) of the in-solve launches of the same
+workload (TRAFFIC_FILES), so ``frac`` = PMC bytes / live duration / 8 TB/s.
+``compulsory_bytes`` is what one launch must move at least (each node image read once,
+its sinogram written once); ``sample_touch`` is SURVEY.md 8d's per-tap accounting, which
+counts LDS-served taps and so exceeds any memory peak -- it is reported as a reuse
+factor, not a rate.  ``step_hbm`` is the whole step's PMC traffic over the measured step
+time.
 
 CPU baseline (``cpu_baseline``): the float64 NumPy/SciPy oracle (oracle/, the port of
 the reference algorithm -- the reference's CVXPY/ODL path cannot run here) doing the
@@ -53,13 +70,14 @@ sys.path.insert(0, os.path.join(ROOT, "distributed-inverse-problem-admm_amd"))
 sys.path.insert(0, ROOT)
 
 N_IMG = 512
-NODES_PER_GPU = 8
+NODES_PER_GPU = 8  # weak-scaling share at N > 1 GPUs
 ANGLES_PER_NODE = 96
 LAM, RHO = 0.02, 2.0
 TV_ITERS, CG_ITERS = 10, 5
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 LDS_PEAK_GBS = 150000.0  # aggregate ds_read_b128 rate, every CU streaming (MI355X_MICROARCH.md, LDS)
 CPU_BASELINE_SECONDS = 8.0  # per-process compute budget of the bounded CPU sample
+XGMI_LINK_GBS, XGMI_LINKS = 153.0, 7  # per direction per link, links per MI355X (task spec)
 
 
 # BASELINE.json configs[1..4]: image side, total graph nodes, graph, dtype, TV
@@ -72,6 +90,16 @@ CONFIGS = {
     # 2048^2 float64 anisotropic x-update (complete graph of the 8 local nodes)
     "C5s": dict(N=2048, nodes=8, graph="complete", dtype="float64", tv="aniso", angles_per_node=96),
 }
+BASELINE_INDEX = {"C2": 1, "C3": 2, "C4": 3, "C5": 4}
+
+
+def workload_cfg(name, world=1):
+    """A BASELINE config, or ``weak8``: 8 nodes per GPU on a ring of 8 x world (512^2, 96
+    angles per node; world = 2 is C3)."""
+    if name == "weak8":
+        return dict(N=N_IMG, nodes=NODES_PER_GPU * world, graph="ring", dtype="float32", tv="iso",
+                    angles_per_node=ANGLES_PER_NODE)
+    return CONFIGS[name]
 
 
 def make_graph(kind, V):
@@ -204,76 +232,73 @@ def cpu_baseline(N, a, b, q, x_gpu, procs=None, budget=CPU_BASELINE_SECONDS):
 # PMC traffic (committed rocprofv3 passes)
 # ---------------------------------------------------------------------------
 # HBM bytes per forward-projector launch and per step from the committed rocprofv3 PMC
-# summary (scripts/pmc.sh + scripts/traffic_summary.py over the launches between the
+# summaries (scripts/pmc.sh + scripts/traffic_summary.py over the launches between the
 # bench's markers, i.e. the timed steps; 2 x FETCH_SIZE + WRITE_SIZE per the
-# MI355X_MICROARCH.md gfx950 correction).  PMC counters cannot be read inside this run.
-TRAFFIC_FILE = "profiles/r3_traffic.json"
+# MI355X_MICROARCH.md gfx950 correction), one per headline workload: the per-launch
+# figure depends on the node chunks one launch projects.  PMC counters cannot be read
+# inside this run.
+TRAFFIC_FILES = {"C3": "profiles/r4_traffic.json", "weak8": "profiles/r4_traffic_weak8.json"}
 FWD_KERNEL = "admm::k_fwdg<float, 8>"
 
 
-def pmc_traffic():
+def pmc_traffic(workload):
+    f = TRAFFIC_FILES.get(workload)
+    if f is None:
+        return None, None
     try:
-        with open(os.path.join(ROOT, TRAFFIC_FILE)) as f:
-            return json.load(f)
+        with open(os.path.join(ROOT, f)) as fh:
+            return json.load(fh), f
     except (OSError, ValueError):
-        return None
+        return None, f
 
 
-def setup_run(cfg_name, world, rank, local_rank):
-    """Operators, sinograms, precisions and the bound node batch of one workload."""
-    import networkx as nx
+def setup_run(name, world, rank, local_rank, exchange=True):
+    """Operators, sinograms, precisions and the bound node batches of rank ``rank`` of a
+    ``world``-rank run of workload ``name``.  ``exchange=False``: no inter-rank exchange (a
+    per-rank proxy on one GPU; halo rows held fixed)."""
     from admm_hip.data import make_precisions, make_sinograms, shepp_logan
-    from admm_hip.exchange import HaloExchange
+    from admm_hip.groups import RankGroups
     from admm_hip.plan import make_plan
-    from admm_hip.solver import NodeBatch, make_operators
-    if cfg_name:
-        cfg = CONFIGS[cfg_name]
-        n_img, V_total, dtype, tv_kind = cfg["N"], cfg["nodes"], cfg["dtype"], cfg["tv"]
-        G = make_graph(cfg["graph"], V_total)
-        angles_total = max(180, 3 * n_img)  # block_2_load_odl_data.py:31-38
-        if "angles_per_node" in cfg:  # a share of a larger config keeps its per-node angle count
-            angles_total = cfg["angles_per_node"] * V_total
-    else:
-        n_img, V_total, dtype, tv_kind = N_IMG, NODES_PER_GPU * world, "float32", "iso"
-        G = nx.cycle_graph(V_total)
-        angles_total = ANGLES_PER_NODE * V_total
+    from admm_hip.solver import make_operators
+    cfg = workload_cfg(name, world)
+    n_img, V_total, dtype, tv_kind = cfg["N"], cfg["nodes"], cfg["dtype"], cfg["tv"]
+    G = make_graph(cfg["graph"], V_total)
+    angles_total = max(180, 3 * n_img)  # block_2_load_odl_data.py:31-38
+    if "angles_per_node" in cfg:  # a share of a larger config keeps its per-node angle count
+        angles_total = cfg["angles_per_node"] * V_total
     ops = make_operators(n_img, V_total, angles_total=angles_total, dtype=dtype, device=local_rank)
     geom = ops[0].geom
-    plan = make_plan(G, V_total, world, rank)
+    local = make_plan(G, V_total, world, rank).local_nodes
     ph = shepp_logan(n_img)
-    lo = plan.local_nodes[0]
-    sinos = dict(zip(plan.local_nodes,
-                     make_sinograms([ops[g] for g in plan.local_nodes], ph, 0.005, seed=1000 + lo)))
+    sinos = dict(zip(local, make_sinograms([ops[g] for g in local], ph, 0.005, seed=1000 + local[0])))
     Wi, Q = make_precisions(ops)  # one W kernel launch: every node shares the geometry
-    nb = NodeBatch(geom, dtype, plan, sinos, Q, RHO, LAM, 10 * LAM, TV_ITERS, CG_ITERS, tv_kind,
-                   ph, local_rank, keep_x=True)
-    halo = HaloExchange(plan, nb.x_ext)
-    return dict(n_img=n_img, V_total=V_total, dtype=dtype, tv_kind=tv_kind, geom=geom, plan=plan,
-                nb=nb, halo=halo, Wi=Wi)
+    rg = RankGroups(ops, G, V_total, world, rank, sinos, Q, RHO, LAM, 10 * LAM, TV_ITERS, CG_ITERS, tv_kind, ph,
+                    keep_x=True, halo=exchange)
+    return dict(name=name, n_img=n_img, V_total=V_total, dtype=dtype, tv_kind=tv_kind, geom=geom, plan=rg.plan,
+                rg=rg, nb=rg.batches[0], Wi=Wi, graph=cfg["graph"])
 
 
-def timed_steps(r, steps, warmup, world, prime=None):
+def timed_steps(r, steps, warmup, world, prime=None, markers=False):
     """Warmup + K timed outer iterations (barrier + synchronize on both sides, max over
-    ranks).  ``prime(nb)`` runs right after the first x-update (before its exchange)."""
+    ranks; ``world`` = this job's process count).  ``prime(nb)`` runs right after the first
+    x-update (before its exchange).  ``markers`` with ADMM_BENCH_MARKERS=1: one marker kernel
+    on each side of the timed steps (scripts/pmc.sh's PMC window)."""
     import torch
     import torch.distributed as dist
-    from admm_hip.exchange import assemble_stats_device
-    nb, halo, plan = r["nb"], r["halo"], r["plan"]
-    E = len(plan.stored_edges)
+    rg = r["rg"]
     host = None
 
     def step(first=False):
         nonlocal host
-        nb.node_update()
+        rg.node_update()
         if first and prime is not None:
-            prime(nb)
-        halo.run()
-        nb.consensus()
+            prime(rg.batches[0])
+        rg.exchange()
+        rg.consensus()
         # the statistics the stop test reads (global table, RCCL all-reduce at N > 1), read
         # back every step into pinned host memory without a per-step host synchronisation --
         # run_admm's pipelined mode (the stop test cannot fire at eps = 0)
-        flat = assemble_stats_device(plan.V_total, len(plan.edges), world,
-                                     [(plan, nb.node_stats, nb.edge_stats[:E])])
+        flat = rg.stats_device() if world > 1 or rg.halo is not None else _stats_local(rg)
         if host is None:
             host = torch.empty(flat.shape, dtype=flat.dtype, pin_memory=True)
         host.copy_(flat, non_blocking=True)
@@ -285,9 +310,9 @@ def timed_steps(r, steps, warmup, world, prime=None):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    marks = os.environ.get("ADMM_BENCH_MARKERS") == "1"
+    marks = markers and os.environ.get("ADMM_BENCH_MARKERS") == "1"
     if marks:
-        nb.marker()
+        rg.batches[0].marker()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
@@ -297,13 +322,90 @@ def timed_steps(r, steps, warmup, world, prime=None):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if marks:
-        nb.marker()
+        rg.batches[0].marker()
         torch.cuda.synchronize()
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     return el
+
+
+def _stats_local(rg):
+    """A proxy rank's statistics table (its own rows of the global one; the W-rank run adds
+    one all-reduce of (V x 8 + E x 3) doubles, which the proxy prices with the exchange)."""
+    from admm_hip.exchange import assemble_stats_device
+    parts = [(nb.plan, nb.node_stats, nb.edge_stats[: len(nb.plan.stored_edges)]) for nb in rg.batches]
+    return assemble_stats_device(rg.plan.V_total, len(rg.plan.edges), 1, parts)
+
+
+# ---------------------------------------------------------------------------
+# per-rank proxies of the multi-GPU runs
+# ---------------------------------------------------------------------------
+def exchange_model(plan, n_img):
+    """Bytes one rank receives per iteration in ``plan``'s exchange and their xGMI time
+    (float64 images; the all-gather moves every rank's padded block, p2p only halo rows)."""
+    npx = n_img * n_img
+    if plan.world == 1:
+        return {"mode": "none", "bytes_received": 0, "peers": 0, "ms_direct": 0.0, "ms_one_link": 0.0}
+    stats_bytes = 8 * (plan.V_total * 8 + len(plan.edges) * 3)  # statistics all-reduce
+    if plan.use_allgather():
+        vmax = max(hi - lo for lo, hi in plan.ranges)
+        recv = (plan.world - 1) * vmax * npx * 8
+        peers = plan.world - 1
+        mode = "allgather"
+    else:
+        recv = sum(len(v) for v in plan.recv.values()) * npx * 8
+        peers = sum(1 for v in plan.recv.values() if v)
+        mode = "p2p"
+    links = max(1, min(peers, XGMI_LINKS))
+    return {"mode": mode, "bytes_received": recv, "peers": peers, "stats_bytes": stats_bytes,
+            "ms_direct": 1e3 * (recv + stats_bytes) / (links * XGMI_LINK_GBS * 1e9),
+            "ms_one_link": 1e3 * (recv + stats_bytes) / (XGMI_LINK_GBS * 1e9)}
+
+
+def busiest_rank(name, world):
+    """The rank of a ``world``-rank run with the most local nodes, then stored edges, then
+    halo rows (the slowest share, which sets the max-over-ranks step time)."""
+    from admm_hip.plan import make_plan
+    cfg = workload_cfg(name, world)
+    G = make_graph(cfg["graph"], cfg["nodes"])
+    best, key = 0, None
+    for r in range(world):
+        p = make_plan(G, cfg["nodes"], world, r)
+        k = (p.V, len(p.stored_edges), len(p.halo_nodes))
+        if key is None or k > key:
+            best, key = r, k
+    return best
+
+
+def time_share(name, world, rank, steps, warmup):
+    """Rank ``rank``'s share of a ``world``-rank run of ``name``, timed on this GPU."""
+    import torch
+    r = setup_run(name, world, rank, 0, exchange=False)
+    el = timed_steps(r, steps, warmup, 1)
+    plan, nb = r["plan"], r["nb"]
+    out = {"rank": rank, "local_nodes": plan.V, "halo_rows": len(plan.halo_nodes),
+           "stored_edges": len(plan.stored_edges), "batches": len(r["rg"].batches), "vb": nb.ctx_vb,
+           "ms_per_step": 1e3 * el / steps, "steps": steps,
+           "exchange": exchange_model(plan, r["n_img"])}
+    del r, nb, plan
+    torch.cuda.empty_cache()
+    return out
+
+
+def proxy(name, world, t1_ms, V_total, steps, warmup):
+    """proxy_8gpu entry of config ``name`` at ``world`` ranks: rank 0's share and the
+    busiest rank's (if different), the exchange, the predicted speedup over one GPU."""
+    ranks = sorted({0, busiest_rank(name, world)})
+    shares = [time_share(name, world, r, steps, warmup) for r in ranks]
+    worst = max(shares, key=lambda s: s["ms_per_step"] + s["exchange"]["ms_direct"])
+    t_d = worst["ms_per_step"] + worst["exchange"]["ms_direct"]
+    t_1 = worst["ms_per_step"] + worst["exchange"]["ms_one_link"]
+    return {"config": name, "ranks": world, "shares": shares, "T1_ms_per_step": t1_ms,
+            "per_node_cost_ratio": (worst["ms_per_step"] / worst["local_nodes"]) / (t1_ms / V_total),
+            "predicted_ms_per_step": t_d, "predicted_speedup": t1_ms / t_d,
+            "predicted_speedup_one_link": t1_ms / t_1}
 
 
 def launch_ranks(n: int) -> int:
@@ -341,98 +443,34 @@ def launch_ranks(n: int) -> int:
     return status
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--fwd-reps", type=int, default=20)
-    ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
-                    help="run a BASELINE.json config (fixed node count) instead of the default workload")
-    ap.add_argument("--strong", default="C4",
-                    help="strong-scaling config measured after the headline ('none' to skip)")
-    ap.add_argument("--strong-steps", type=int, default=3)
-    args = ap.parse_args()
-    if args.gpus < 1:
-        ap.error("--gpus must be >= 1")
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(launch_ranks(args.gpus))  # decided before any GPU call of this process
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus:
-        ap.error(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU, they must match")
-
-    import torch
-    import torch.distributed as dist
-
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; ADMM_DIST_BACKEND=gloo (+ more ranks than GPUs) is a 1-GPU
-    # rehearsal of the sharded path only -- the measured configuration is nccl (RCCL)
-    backend = os.environ.get("ADMM_DIST_BACKEND", "nccl")
-    local_rank = local_rank % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        else:
-            dist.init_process_group(backend)
-
-    r = setup_run(args.config, world, rank, local_rank)
-    if world > 1:
-        dist.barrier()
-    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and not args.config
-    first = {}
-
-    def prime(nb):  # node 0's first x-update and its inputs, for the CPU parity check
-        if want_cpu:
-            first["x"] = nb.x_local[0].to("cpu").numpy().copy()
-            first["b"] = nb.b[0].to("cpu").double().numpy().copy()
-
-    el = timed_steps(r, args.steps, args.warmup, world, prime)
-    nb, plan, geom = r["nb"], r["plan"], r["geom"]
-    # N > 1: the halo rows the last exchange delivered (RCCL p2p / all-gather) must equal the
-    # owners' images byte for byte (checked after the timed region)
-    from admm_hip.exchange import verify_halo
-    xcheck = verify_halo(plan, nb.x_ext) if world > 1 else None
-    n_img, V_total, dtype = r["n_img"], r["V_total"], r["dtype"]
-    value = V_total * args.steps / el
-    ms_per_step = 1e3 * el / args.steps
-
-    # live measurement of the dominant kernel (forward projector taps) on its stream: HIP events
-    # around every CG-step forward of one more x-update (after the timed region and the halo
-    # check), each launch right after the CG / TV update that wrote its image, as in the timed
-    # steps -- the figure rocprofv3's in-solve average must agree with; back-to-back launches,
-    # which find the image rows still in L2, are reported beside it
+def forward_roofline(r, workload, fwd_reps):
+    """``roofline`` of the dominant kernel (forward taps) of a bound workload: live HIP-event
+    timing of its in-solve launches, PMC bytes from the committed passes of that workload."""
+    nb, geom, plan = r["nb"], r["geom"], r["plan"]
+    # HIP events around every CG-step forward of one more x-update (after the timed region
+    # and the halo check), each launch right after the CG / TV update that wrote its image, as
+    # in the timed steps -- the figure rocprofv3's in-solve average must agree with;
+    # back-to-back launches, which find the image rows still in L2, are reported beside it
     fwd_ms = nb.time_forward(in_solve=True)
-    fwd_ms_warm = nb.time_forward(args.fwd_reps)
+    fwd_ms_warm = nb.time_forward(fwd_reps)
+    n_img, dtype = r["n_img"], r["dtype"]
     a_node = geom.n_angles
     sbytes = 8 if dtype == "float64" else 4
-    B_A, B_At, B_node = sample_touch_bytes(n_img, a_node, TV_ITERS, CG_ITERS, sbytes)
-    V = plan.V
+    B_A, _, _ = sample_touch_bytes(n_img, a_node, TV_ITERS, CG_ITERS, sbytes)
+    V = nb.V
     n, m = n_img * n_img, a_node * n_img
     compulsory = V * n * sbytes + V * m * sbytes  # each node image read once, its sinogram written once
     as_designed = 2 * V * n * sbytes + 8 * V * m * sbytes  # image + transposed copy, 8 segment partials
     lds_bytes = sbytes * a_node * n_img * 2 * n_img * V  # m rays x N rows x 2 taps x V samples
-    # per-launch PMC bytes of the forward kernel: every rank runs the same 8-node launch, so the
-    # 1-GPU passes apply at any rank count (the per-step figure below is 1-GPU only: halo traffic)
-    tr = pmc_traffic() if not args.config else None
+    tr, tr_file = pmc_traffic(workload)
     fwd_traffic = tr["kernels"].get(FWD_KERNEL, {}).get("hbm_bytes_per_launch") if tr else None
-    if args.config:
-        workload = (f"{args.config}: {n_img}^2, {V_total} graph nodes ({CONFIGS[args.config]['graph']}), "
-                    f"{a_node} angles/node, {dtype} samples, {r['tv_kind']} TV, lam=0.02 rho=2, "
-                    f"split-Bregman {TV_ITERS}x{CG_ITERS} CG, one step = one outer ADMM iteration")
-    else:
-        workload = (f"512^2, {NODES_PER_GPU} graph nodes/GPU x {ANGLES_PER_NODE} angles (ring of "
-                    f"{V_total}; N=2 == BASELINE configs[2]), lam=0.02 rho=2, split-Bregman "
-                    f"{TV_ITERS}x{CG_ITERS} CG, one step = one outer ADMM iteration")
     fwd_s = fwd_ms * 1e-3
     roof = {
         "kernel": f"k_fwdg<{'double' if dtype == 'float64' else 'float'},{nb.ctx_vb}> (Joseph forward "
-                  "projector taps, angle-grouped, 8 row-segment partial sums per ray)",
+                  f"projector taps, angle-grouped, 8 row-segment partial sums per ray; {V} nodes = "
+                  f"{-(-V // nb.ctx_vb)} node chunk(s) per launch)",
         # the angle-group plan the batch bound (admm_fwd_plan_info): 0 = 64-ray chunks,
-        # 1 = aligned per (segment, angle), 2 = aligned per (segment, chunk)
+        # 1 = aligned per (segment, angle), 2 = aligned per (segment, chunk); 3-5 = clipped
         "fwd_plan": next((dict(p) for p in nb.fwd_plans() if p["active"]), None),
         "bound": "hbm",
         "achieved": fwd_traffic / fwd_s / 1e9 if fwd_traffic is not None else None,
@@ -440,8 +478,8 @@ def main():
         "unit": "GB/s",
         "frac": fwd_traffic / fwd_s / 1e9 / HBM_PEAK_GBS if fwd_traffic is not None else None,
         "traffic": fwd_traffic,
-        "traffic_source": (f"{TRAFFIC_FILE}: rocprofv3 PMC 2 x FETCH_SIZE + WRITE_SIZE per in-solve "
-                           "launch (Infinity-Cache hits included)") if fwd_traffic is not None else None,
+        "traffic_source": (f"{tr_file}: rocprofv3 PMC 2 x FETCH_SIZE + WRITE_SIZE per in-solve launch "
+                           "(Infinity-Cache hits included)") if fwd_traffic is not None else None,
         "avg_launch_ms": fwd_ms,
         "avg_launch_ms_back_to_back": fwd_ms_warm,
         "compulsory_bytes": compulsory,
@@ -470,6 +508,126 @@ def main():
     }
     if roof["frac"] is not None:
         assert roof["frac"] <= 1.0, roof
+    return roof, tr, tr_file
+
+
+def describe(r, world):
+    name = r["name"]
+    if name == "weak8":
+        return (f"512^2, {NODES_PER_GPU} graph nodes/GPU x {ANGLES_PER_NODE} angles (ring of {r['V_total']}; "
+                f"N=2 == BASELINE configs[2]), lam=0.02 rho=2, split-Bregman {TV_ITERS}x{CG_ITERS} CG, one step "
+                f"= one outer ADMM iteration")
+    idx = BASELINE_INDEX.get(name)
+    tag = f"BASELINE.json configs[{idx}] " if idx is not None else ""
+    return (f"{name} ({tag}{r['n_img']}^2, {r['V_total']} graph nodes ({r['graph']}), {r['geom'].n_angles} "
+            f"angles/node, {r['dtype']} samples, {r['tv_kind']} TV, lam=0.02 rho=2, split-Bregman "
+            f"{TV_ITERS}x{CG_ITERS} CG) on {world} GPU(s), one step = one outer ADMM iteration")
+
+
+def leg(name, world, rank, local_rank, steps, warmup):
+    """A fixed-size config sharded over this job's ranks (strong scaling), measured."""
+    import torch
+    import torch.distributed as dist
+    r = setup_run(name, world, rank, local_rank)
+    if world > 1:
+        dist.barrier()
+    el = timed_steps(r, steps, warmup, world)
+    out = {"config": name, "scaling": "strong" if name != "weak8" else "weak", "workload": describe(r, world),
+           "nodes": r["V_total"], "value": r["V_total"] * steps / el, "unit": "node-updates/s",
+           "ms_per_step": 1e3 * el / steps, "steps": steps, "warmup": warmup}
+    del r
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fwd-reps", type=int, default=20)
+    ap.add_argument("--workload", choices=("auto", "C3", "weak8"), default="auto",
+                    help="headline: auto = C3 on one GPU, weak8 (8 nodes per GPU) on N > 1")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
+                    help="run a BASELINE.json config (fixed node count) instead of the headline workload")
+    ap.add_argument("--as-rank", default=None, metavar="R/W",
+                    help="with --config: time rank R's share of a W-rank run on this one GPU (proxy)")
+    ap.add_argument("--strong", default=None,
+                    help="strong-scaling configs measured after the headline, comma separated "
+                         "(default: C4 on one GPU, C3,C4 on N > 1; 'none' to skip)")
+    ap.add_argument("--strong-steps", type=int, default=3)
+    ap.add_argument("--proxy", choices=("none", "fast", "all"), default="fast",
+                    help="one GPU only: per-rank proxies of the multi-GPU runs (fast: C3 on 2, C4 on 2/4/8 "
+                         "ranks; all: + C5 on 8 ranks, which also times C5 on one GPU)")
+    ap.add_argument("--proxy-steps", type=int, default=3)
+    ap.add_argument("--headline-only", action="store_true",
+                    help="only the headline workload (no weak8, strong or proxy legs): rocprofv3 runs")
+    args = ap.parse_args()
+    if args.headline_only:
+        args.strong, args.proxy = "none", "none"
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.as_rank is not None and args.config is None:
+        ap.error("--as-rank needs --config")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))  # decided before any GPU call of this process
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        ap.error(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU, they must match")
+
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; ADMM_DIST_BACKEND=gloo (+ more ranks than GPUs) is a 1-GPU
+    # rehearsal of the sharded path only -- the measured configuration is nccl (RCCL)
+    backend = os.environ.get("ADMM_DIST_BACKEND", "nccl")
+    local_rank = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
+
+    if args.as_rank is not None:  # one rank's share on this GPU, as its own line
+        if world != 1:
+            ap.error("--as-rank is a one-GPU measurement")
+        R, W = (int(v) for v in args.as_rank.split("/"))
+        if not (0 <= R < W):
+            ap.error("--as-rank R/W needs 0 <= R < W")
+        sh = time_share(args.config, W, R, args.steps, args.warmup)
+        print(json.dumps({"metric": "per-rank share (proxy): ms per outer ADMM iteration", "value": sh["ms_per_step"],
+                          "unit": "ms/step", "higher_is_better": False, "n_gpus": 1, "config": args.config,
+                          "as_rank": args.as_rank, "share": sh}))
+        return
+
+    workload = args.config or (args.workload if args.workload != "auto" else ("C3" if world == 1 else "weak8"))
+    r = setup_run(workload, world, rank, local_rank)
+    if world > 1:
+        dist.barrier()
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and workload in ("C3", "weak8")
+    first = {}
+
+    def prime(nb):  # node 0's first x-update and its inputs, for the CPU parity check
+        if want_cpu:
+            first["x"] = nb.x_local[0].to("cpu").numpy().copy()
+            first["b"] = nb.b[0].to("cpu").double().numpy().copy()
+
+    el = timed_steps(r, args.steps, args.warmup, world, prime, markers=True)
+    plan, geom = r["plan"], r["geom"]
+    # N > 1: the halo rows the last exchange delivered (RCCL p2p / all-gather) must equal the
+    # owners' images byte for byte (checked after the timed region)
+    from admm_hip.exchange import verify_halo
+    xcheck = verify_halo(plan, r["rg"].x_rank) if world > 1 else None
+    n_img, V_total, dtype = r["n_img"], r["V_total"], r["dtype"]
+    value = V_total * args.steps / el
+    ms_per_step = 1e3 * el / args.steps
+    roof, tr, tr_file = forward_roofline(r, workload, args.fwd_reps)
+    headline_fixed = workload in CONFIGS  # a fixed-size config (C3 headline, --config)
     result = {
         "metric": "ADMM node-updates/sec (whole node), 512² phantom; rel-Fro vs CPU ref",
         "value": value,
@@ -479,45 +637,63 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "strong" if args.config else "weak",
+        "scaling": "strong" if headline_fixed else "weak",
         "vs_baseline": None,
         "dtype": ("f64 samples / f64 state" if dtype == "float64" else "f32 samples / f64 state"),
         "data": "synthetic modified Shepp-Logan, on-GPU Gaussian noise sigma=0.005",
         "config": {
-            "workload": workload,
-            "image": n_img, "nodes": V_total, "angles_per_node": a_node,
-            "graph": CONFIGS[args.config]["graph"] if args.config else "ring",
+            "workload": describe(r, world),
+            "baseline_config": BASELINE_INDEX.get(workload),
+            "image": n_img, "nodes": V_total, "angles_per_node": geom.n_angles,
+            "graph": r["graph"],
             "parallelism": f"graph-node shards x{world}",
         },
         "roofline": roof,
     }
     if xcheck is not None:
-        result["exchange_check"] = dict(xcheck, backend=backend, mode=r["halo"].mode,
+        result["exchange_check"] = dict(xcheck, backend=backend, mode=r["rg"].halo.mode,
                                         ok=xcheck["mismatched_rows"] == 0)
-    if tr and tr.get("per_step") and not args.config and world == 1:
+    if tr and tr.get("per_step") and world == 1:
         sb = float(tr["per_step"]["hbm_bytes"])
         gbs = sb / (ms_per_step * 1e-3) / 1e9
         assert gbs <= HBM_PEAK_GBS, (sb, ms_per_step)
         result["step_hbm"] = {"bytes": sb, "achieved_gbs": gbs, "frac": gbs / HBM_PEAK_GBS,
-                              "source": f"{TRAFFIC_FILE} per_step (PMC, timed steps between markers)"}
+                              "source": f"{tr_file} per_step (PMC, timed steps between markers)"}
     if want_cpu and "x" in first:
-        result["cpu_baseline"] = cpu_baseline(n_img, a_node, first["b"], r["Wi"][0], first["x"])
-    # strong scaling: a fixed BASELINE config sharded over the same ranks
-    if args.strong and args.strong.lower() != "none" and not args.config:
-        del r, nb
-        torch.cuda.empty_cache()
-        rs = setup_run(args.strong, world, rank, local_rank)
+        result["cpu_baseline"] = cpu_baseline(n_img, geom.n_angles, first["b"], r["Wi"][0], first["x"])
+    del r
+    torch.cuda.empty_cache()
+    if args.config:
+        if rank == 0:
+            print(json.dumps(result))
         if world > 1:
-            dist.barrier()
-        els = timed_steps(rs, args.strong_steps, 1, world)
-        result["strong"] = {
-            "config": args.strong, "scaling": "strong",
-            "workload": f"{rs['n_img']}^2, {rs['V_total']} graph nodes ({CONFIGS[args.strong]['graph']}), "
-                        f"{rs['geom'].n_angles} angles/node, {rs['dtype']} samples, fixed total work "
-                        f"sharded over {world} rank(s)",
-            "value": rs["V_total"] * args.strong_steps / els, "unit": "node-updates/s",
-            "ms_per_step": 1e3 * els / args.strong_steps, "steps": args.strong_steps, "warmup": 1,
-        }
+            dist.destroy_process_group()
+        return
+    # the 8-nodes-per-GPU share of the N > 1 runs, on one GPU
+    if world == 1 and workload != "weak8" and not args.headline_only:
+        result["weak8"] = leg("weak8", 1, 0, local_rank, args.steps, args.warmup)
+    # strong scaling: fixed BASELINE configs sharded over the same ranks
+    strong = args.strong if args.strong is not None else ("C4" if world == 1 else "C3,C4")
+    legs = [c for c in strong.split(",") if c and c.lower() != "none"]
+    result["strong"] = [leg(c, world, rank, local_rank, args.strong_steps, 1) for c in legs]
+    # per-rank proxies of the multi-GPU runs (one GPU): each share timed here, exchange priced
+    if world == 1 and args.proxy != "none":
+        t1 = {"C3": (V_total, ms_per_step)} if workload == "C3" else {}
+        for s in result["strong"]:
+            t1[s["config"]] = (s["nodes"], s["ms_per_step"])
+        todo = [("C3", 2), ("C4", 2), ("C4", 4), ("C4", 8)] + ([("C5", 8)] if args.proxy == "all" else [])
+        px = {}
+        for name, W in todo:
+            if name not in t1:
+                s = leg(name, 1, 0, local_rank, 2 if name == "C5" else args.strong_steps, 1)
+                t1[name] = (s["nodes"], s["ms_per_step"])
+            V, t = t1[name]
+            px[f"{name}@{W}"] = proxy(name, W, t, V, args.proxy_steps, 1)
+        result["proxy_8gpu"] = dict(
+            px, model=f"T_rank = rank's share timed on this GPU (halo rows fixed); exchange = bytes received "
+                      f"(float64 images + statistics) over xGMI, direct = min(peers, {XGMI_LINKS}) links x "
+                      f"{XGMI_LINK_GBS:.0f} GB/s, one_link = a single link; predicted_speedup = T_1 / "
+                      f"(T_rank + exchange_direct); the exchange is not overlapped with compute")
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

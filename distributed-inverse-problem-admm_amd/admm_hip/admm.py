@@ -53,6 +53,7 @@ EXTRA_KEYS = ("sb_res_history", "inner_updates_history")
 
 DEFAULT_MU_FACTOR = 10.0  # split-Bregman penalty mu = 10 * lam_tv
 EPS_CAP, CALIB_ALPHA, MAX_TIGHTEN = 1e-2, 1.0, 2  # block_6_admm_loop_ver2.py:106-113
+PIPELINE_BLOCK = 64  # iterations of statistics held on the device in the pipelined mode
 
 
 def eps_target(k: int) -> float:
@@ -94,7 +95,10 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
     (tests check the edge invariants on the device arrays).  ``pipeline``: read the
     statistics back once after the loop instead of every iteration (default: whenever the
     stop test cannot fire and no per-iteration host output is requested; False forces the
-    per-iteration read-back)."""
+    per-iteration read-back).  In the pipelined mode the device keeps the statistics of at most
+    ``PIPELINE_BLOCK`` iterations (V_total x 8 + E x 3 float64 each) and flushes them to the host
+    every ``PIPELINE_BLOCK`` iterations, so the verbose progress lines of those iterations are
+    printed at each flush (and at the end), not as each iteration finishes."""
     if inner_tol not in (None, "reference"):
         raise ValueError("inner_tol must be None (fixed counts) or 'reference'")
     if inner_chunks is not None:
@@ -147,6 +151,7 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
     pipelined = ((eps_pri <= 0 or eps_dual <= 0) and inner_tol is None and snapshot_dir is None
                  and chunk_snapshot_dir is None and pipeline is not False)
     dev_hist = None
+    flushed = 0  # iterations of the pipelined statistics already recorded on the host
     for k in range(max_iters):
         et = eps_target(k)
         if inner_chunks is None:
@@ -168,8 +173,12 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
         if pipelined:
             flat = rg.stats_device()
             if dev_hist is None:
-                dev_hist = torch.empty((max_iters, flat.numel()), dtype=torch.float64, device=flat.device)
-            dev_hist[k].copy_(flat)
+                dev_hist = torch.empty((min(max_iters, PIPELINE_BLOCK), flat.numel()), dtype=torch.float64,
+                                       device=flat.device)
+            dev_hist[k - flushed].copy_(flat)
+            if k + 1 - flushed == dev_hist.shape[0]:  # block full: flush to the host
+                flushed = _flush_pipelined(hist, dev_hist, flushed, k + 1, rg, V_total, edges, rho, lam_tv,
+                                           have_ph, verbose and rank == 0)
             continue
         ns, es = rg.stats(np.stack([eps_used, n_upd], axis=1))
         pn, dn = _record(hist, ns.numpy(), es.numpy(), edges, V_total, rho, lam_tv, et, have_ph)
@@ -181,16 +190,9 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
             if verbose and rank == 0:
                 print(f"stopped at iter {k}, primal {pn:.3e}, dual {dn:.3e}")
             break
-    if pipelined and dev_hist is not None:
-        host = dev_hist[:iters_done].to("cpu")
-        nsw = rg.batches[0].node_stats.shape[1]
-        extra = np.stack([np.full(V_total, np.nan), np.ones(V_total)], axis=1)
-        for k in range(iters_done):
-            ns, es = split_stats(host[k], V_total, nsw, len(edges), rg.batches[0].edge_stats.shape[1])
-            pn, dn = _record(hist, np.concatenate([ns.numpy(), extra], axis=1), es.numpy(), edges, V_total,
-                             rho, lam_tv, eps_target(k), have_ph)
-            if verbose and rank == 0 and k % 10 == 0:
-                print(f"iter {k}, primal {pn:.3e}, dual {dn:.3e}")
+    if pipelined and dev_hist is not None and iters_done > flushed:
+        flushed = _flush_pipelined(hist, dev_hist, flushed, iters_done, rg, V_total, edges, rho, lam_tv, have_ph,
+                                   verbose and rank == 0)
     torch.cuda.synchronize()
     if timing is not None:
         import time
@@ -206,6 +208,21 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
         return [X[i] for i in range(V_total)], hist
     Xh = X.to("cpu").numpy()
     return [Xh[i].copy() for i in range(V_total)], hist
+
+
+def _flush_pipelined(hist, dev_hist, k0, k1, rg, V_total, edges, rho, lam_tv, have_ph, verbose):
+    """Record iterations k0 .. k1-1 of the pipelined statistics (rows 0 .. k1-k0-1 of
+    ``dev_hist``) on the host; returns k1."""
+    host = dev_hist[: k1 - k0].to("cpu")
+    nsw = rg.batches[0].node_stats.shape[1]
+    extra = np.stack([np.full(V_total, np.nan), np.ones(V_total)], axis=1)
+    for k in range(k0, k1):
+        ns, es = split_stats(host[k - k0], V_total, nsw, len(edges), rg.batches[0].edge_stats.shape[1])
+        pn, dn = _record(hist, np.concatenate([ns.numpy(), extra], axis=1), es.numpy(), edges, V_total,
+                         rho, lam_tv, eps_target(k), have_ph)
+        if verbose and k % 10 == 0:
+            print(f"iter {k}, primal {pn:.3e}, dual {dn:.3e}")
+    return k1
 
 
 def _record(hist, ns, es, edges, V_total, rho, lam_tv, et, have_ph):

@@ -10,8 +10,8 @@ ones (/root/reference/block_2_load_odl_data.py:31-38) -- its own defaults give
 
 ``RankGroups`` therefore splits the rank's nodes by operator key (geometry or matrix
 digest, sample dtype, device) into node batches (``NodeBatch``, each with a subset plan,
-plan.make_subset_plan).  A group larger than one batch may hold (max_batch_nodes: 63 nodes
-at 2048^2) is split into several batches the same way.  With one batch -- every BASELINE
+plan.make_subset_plan).  A group larger than one batch may hold (max_batch_nodes: 56 nodes
+at 2048^2) is split into several batches the same way (C5's 64 nodes on one GPU: 56 + 8).  With one batch -- every BASELINE
 config at its GPU count -- the batch IS the rank:
 its ``x_ext`` is exchanged in place and nothing else runs.  With several, an edge between
 two groups is stored by both and updated bitwise identically at both (the single-y /
@@ -38,8 +38,8 @@ def operator_key(A):
 def max_batch_nodes(geom) -> int:
     """Most nodes one device batch may hold: the library addresses a batch's node-interleaved
     sample buffers with 32-bit offsets (admm_batch_bind: V x max(n, m) x 8 bytes < 2^31), so
-    at 2048^2 (n = 4.2 M) a batch holds at most 63 nodes -- C5's 64 on one GPU are two
-    batches.  Rounded down to whole 8-node chunks (the widest interleave)."""
+    at 2048^2 (n = 4.2 M) that is 63 nodes, rounded down to whole 8-node chunks (the widest
+    interleave): 56."""
     cap = ((1 << 31) - 1) // (8 * max(geom.n, geom.m))
     return cap - cap % 8 if cap >= 8 else max(1, cap)
 
@@ -47,8 +47,12 @@ def max_batch_nodes(geom) -> int:
 class RankGroups:
     def __init__(self, A_list, G, V_total: int, world: int, rank: int, sinograms, Qij_diag_fn,
                  rho, lam, mu, tv_iters, cg_iters, tv_kind, phantom, fusion="midpoint", Wi_list=None,
-                 keep_x=False, group=None):
+                 keep_x=False, group=None, halo=True):
+        """``halo=False``: no inter-rank exchange (bench.py's per-rank proxy: one rank's share
+        of a ``world``-rank run on one GPU, its halo rows held fixed)."""
         self.plan: ShardPlan = make_plan(G, V_total, world, rank)
+        if not self.plan.local_nodes:
+            raise ValueError(f"rank {rank} owns no graph nodes ({V_total} nodes over {world} ranks)")
         self.world = world
         self.group = group
         keys, members = [], {}
@@ -58,7 +62,12 @@ class RankGroups:
                 keys.append(k)
                 members[k] = []
             members[k].append(g)
-        # groups larger than one batch may hold are split into consecutive chunks
+        # groups larger than one batch may hold are split into consecutive cap-sized chunks.
+        # Not near-equal: every edge between two batches is stored (and updated) by both, and
+        # for a dense graph the cross edges |A| x |B| are fewest for the most unequal split --
+        # C5 on one GPU as 56 + 8 stores 2464 edges, as 32 + 32 it would store 3040 (+36 GB of
+        # float64 edge state); at 2048^2 an 8-node batch is two 4-node chunks of 1816 forward
+        # blocks each, so the small batch does not idle the GPU
         split = []
         for k in keys:
             cap = max_batch_nodes(k[0])
@@ -94,7 +103,7 @@ class RankGroups:
             # (batch, its local rows' slots in x_rank, x_rank slots of its halo rows)
             self.moves = [(nb, lt([row[g] for g in nb.plan.local_nodes]), lt([row[g] for g in nb.plan.halo_nodes]))
                           for nb in self.batches]
-        self.halo = HaloExchange(self.plan, self.x_rank, group)
+        self.halo = HaloExchange(self.plan, self.x_rank, group) if halo else None
 
     @property
     def single(self) -> bool:
@@ -113,7 +122,8 @@ class RankGroups:
         this rank, other ranks)."""
         for nb, loc, _ in self.moves:
             self.x_rank.index_copy_(0, loc, nb.x_local)
-        self.halo.run()
+        if self.halo is not None:
+            self.halo.run()
         for nb, _, hal in self.moves:
             if hal.numel():
                 torch.index_select(self.x_rank, 0, hal, out=nb.x_ext[nb.V:])

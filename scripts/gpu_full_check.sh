@@ -12,7 +12,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 200 --timeou
 rc=$?; echo "pytest rc=$rc"; tail -14 gpurun_out/pytest_$TAG.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --strong none > gpurun_out/prof_$TAG.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --headline-only > gpurun_out/prof_$TAG.log 2>&1
 rc=$?; echo "rocprof rc=$rc"
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err

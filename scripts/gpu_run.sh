@@ -1,0 +1,54 @@
+#!/bin/bash
+# One parameterised GPU session (replaces the numbered one-off scripts of round 3).
+# usage: bash scripts/gpu_run.sh TAG STEP [STEP ...]
+#   pmc        PMC HBM passes of the C3 headline and the weak8 share -> profiles/TAG_traffic*.json
+#   tests=EXPR pytest -m gpu -k EXPR (EXPR "all": every gpu test)
+#   prof       rocprofv3 --kernel-trace --stats of the headline -> gpurun_out/prof_TAG
+#   bench      the default bench line (CPU baseline, weak8, strong C4, proxies fast)
+#   benchall   the default bench line with --proxy all (adds C5 on 8 ranks and C5 on one GPU)
+#   configs    bench.py --config C2 C3 C4 C5s
+#   smoke      __graft_entry__.smoke()
+# Every step has its own time limit; the first failing step ends the session.
+set -u
+mkdir -p gpurun_out
+TAG=$1; shift
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+run() {  # name, limit, command...
+  local name=$1 lim=$2; shift 2
+  echo "== $name"
+  timeout -k 10 $lim "$@"
+  local rc=$?
+  echo "== $name rc=$rc"
+  return $rc
+}
+for step in "$@"; do
+  case $step in
+    pmc)
+      run pmc_c3 400 bash scripts/pmc.sh ${TAG} > gpurun_out/pmc_${TAG}.log 2>&1 || { tail -5 gpurun_out/pmc_${TAG}.log; exit 1; }
+      cp gpurun_out/${TAG}_traffic.json profiles/${TAG}_traffic.json
+      WORKLOAD=weak8 run pmc_weak8 400 bash scripts/pmc.sh ${TAG}w8 > gpurun_out/pmc_${TAG}w8.log 2>&1 || { tail -5 gpurun_out/pmc_${TAG}w8.log; exit 1; }
+      cp gpurun_out/${TAG}w8_traffic.json profiles/${TAG}_traffic_weak8.json
+      tail -12 gpurun_out/pmc_${TAG}.log ;;
+    tests=*)
+      expr=${step#tests=}
+      if [ "$expr" = all ]; then k=(); else k=(-k "$expr"); fi
+      run pytest 1100 python -u -m pytest tests -m gpu "${k[@]}" -q -rf --timeout 600 --timeout-method thread --durations=15 > gpurun_out/pytest_${TAG}.log 2>&1
+      rc=$?; tail -25 gpurun_out/pytest_${TAG}.log; [ $rc -ne 0 ] && exit $rc ;;
+    prof)
+      run prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --headline-only > gpurun_out/prof_${TAG}.log 2>&1 || exit 1
+      python scripts/top_kernels.py gpurun_out/prof_${TAG} ;;
+    bench)
+      run bench 600 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || { tail -5 gpurun_out/bench_${TAG}.err; exit 1; }
+      python scripts/summarize_bench.py gpurun_out/bench_${TAG}.json ;;
+    benchall)
+      run benchall 900 python bench.py --steps 20 --warmup 5 --proxy all > gpurun_out/benchall_${TAG}.json 2> gpurun_out/benchall_${TAG}.err || { tail -5 gpurun_out/benchall_${TAG}.err; exit 1; }
+      python scripts/summarize_bench.py gpurun_out/benchall_${TAG}.json ;;
+    configs)
+      run configs 1000 bash scripts/run_configs.sh C2 C3 C4 C5s || exit 1 ;;
+    smoke)
+      run smoke 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke_${TAG}.log 2>&1
+      rc=$?; tail -2 gpurun_out/smoke_${TAG}.log; [ $rc -ne 0 ] && exit $rc ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+exit 0

@@ -12,8 +12,8 @@ import bench  # noqa: E402
 from admm_hip.exchange import assemble_stats  # noqa: E402
 
 torch.cuda.set_device(0)
-r = bench.setup_run(None, 1, 0, 0)
-nb, halo, plan = r["nb"], r["halo"], r["plan"]
+r = bench.setup_run("weak8", 1, 0, 0)
+nb, halo, plan = r["nb"], r["rg"].halo, r["plan"]
 E = len(plan.stored_edges)
 hs = torch.empty(nb.node_stats.shape, dtype=torch.float64, pin_memory=True)
 he = torch.empty((max(E, 1), nb.edge_stats.shape[1]), dtype=torch.float64, pin_memory=True)

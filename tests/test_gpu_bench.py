@@ -21,12 +21,17 @@ def _run(*args, env=None):
 
 
 def test_bench_line_contract(cuda):
-    b = _run("--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--strong", "none")
+    b = _run("--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--strong", "none", "--proxy", "none")
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
               "scaling", "vs_baseline", "dtype", "data", "config", "roofline"):
         assert k in b, k
     assert b["n_gpus"] == 1 and b["steps"] == 3 and b["warmup"] == 1
-    assert b["unit"] == "node-updates/s" and b["higher_is_better"] is True and b["scaling"] == "weak"
+    assert b["unit"] == "node-updates/s" and b["higher_is_better"] is True
+    # one GPU: the headline is BASELINE configs[2] itself (C3: 16-node ring at 512^2), a fixed
+    # config; the 8-nodes-per-GPU share of the N > 1 weak-scaling runs rides along as weak8
+    assert b["config"]["nodes"] == 16 and b["config"]["baseline_config"] == 2 and b["scaling"] == "strong"
+    assert "configs[2]" in b["config"]["workload"] and b["config"]["angles_per_node"] == 96
+    assert b["weak8"]["nodes"] == 8 and b["weak8"]["value"] > 0 and b["strong"] == []
     # value = node-updates of the whole job / timed wall time
     assert abs(b["value"] - b["config"]["nodes"] * 1e3 / b["ms_per_step"]) <= 1e-6 * b["value"]
     r = b["roofline"]
@@ -46,24 +51,54 @@ def test_bench_launches_its_own_ranks(cuda):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["ADMM_DIST_BACKEND"] = "gloo"
     b = _run("--gpus", "2", "--steps", "2", "--warmup", "1", "--strong", "none", env=env)
-    assert b["n_gpus"] == 2 and b["config"]["nodes"] == 16
+    assert b["n_gpus"] == 2 and b["config"]["nodes"] == 16 and b["scaling"] == "weak"
     assert b["exchange_check"]["ok"] and b["exchange_check"]["halo_rows"] == 4
 
 
 @pytest.mark.timeout(600)
 def test_bench_eight_ranks_with_strong_c4(cuda):
-    """The driver's N = 8 command shape (``bench.py --gpus 8``, default strong leg C4) as a
-    gloo rehearsal on this one GPU: 64-node ring over 8 self-launched ranks, then C4's
-    32-node ER graph over the same 8 ranks (all-gather exchange on every rank)."""
+    """The driver's N = 8 command shape (``bench.py --gpus 8``, default strong legs C3, C4) as
+    a gloo rehearsal on this one GPU: 64-node ring over 8 self-launched ranks, then C3's
+    16-node ring (2 nodes per rank) and C4's 32-node ER graph (all-gather exchange on every
+    rank) over the same 8 ranks."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["ADMM_DIST_BACKEND"] = "gloo"
     b = _run("--gpus", "8", "--steps", "1", "--warmup", "1", "--strong-steps", "1", env=env)
     assert b["n_gpus"] == 8 and b["config"]["nodes"] == 64
     assert b["exchange_check"]["ok"] and b["exchange_check"]["mode"] == "p2p"
-    assert b["strong"]["config"] == "C4" and b["strong"]["value"] > 0
+    assert [s["config"] for s in b["strong"]] == ["C3", "C4"]
+    assert all(s["value"] > 0 and s["scaling"] == "strong" for s in b["strong"])
 
 
 def test_bench_config_line(cuda):
     b = _run("--config", "C2", "--steps", "2", "--warmup", "1")
     assert b["scaling"] == "strong" and b["config"]["nodes"] == 8 and b["config"]["image"] == 256
     assert b["value"] > 0
+
+
+def test_bench_as_rank_share(cuda):
+    """``--config C4 --as-rank 0/8``: rank 0's share of C4 on 8 GPUs bound on this GPU --
+    4 local nodes (one batch at node-interleave width 4), its real halo rows and stored
+    edges of the 103-edge ER graph, all-gather exchange priced, not run."""
+    b = _run("--config", "C4", "--as-rank", "0/8", "--steps", "2", "--warmup", "1")
+    sh = b["share"]
+    assert b["unit"] == "ms/step" and b["value"] == sh["ms_per_step"] > 0
+    assert sh["local_nodes"] == 4 and sh["vb"] == 4 and sh["batches"] == 1 and sh["rank"] == 0
+    assert sh["halo_rows"] > 0 and sh["stored_edges"] > 0
+    assert sh["exchange"]["mode"] == "allgather" and sh["exchange"]["bytes_received"] == 7 * 4 * 1024 * 1024 * 8
+
+
+@pytest.mark.timeout(600)
+def test_bench_default_proxies(cuda):
+    """The default one-GPU line's per-rank proxies: C3 on 2 ranks, C4 on 2 / 4 / 8 ranks, each
+    with its measured one-GPU time, the share's time and the predicted speedup."""
+    b = _run("--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--strong-steps", "1", "--proxy-steps", "1")
+    px = b["proxy_8gpu"]
+    assert set(k for k in px if "@" in k) == {"C3@2", "C4@2", "C4@4", "C4@8"}
+    assert [s["config"] for s in b["strong"]] == ["C4"]
+    for k in ("C3@2", "C4@2", "C4@4", "C4@8"):
+        p = px[k]
+        assert p["T1_ms_per_step"] > 0 and p["predicted_speedup"] > 0 and p["per_node_cost_ratio"] > 0
+        assert all(s["ms_per_step"] > 0 for s in p["shares"])
+    assert px["C3@2"]["T1_ms_per_step"] == b["ms_per_step"]  # the headline is C3 on this GPU
+    assert px["C4@8"]["shares"][0]["vb"] == 4 and px["C3@2"]["shares"][0]["exchange"]["mode"] == "p2p"
