@@ -252,6 +252,9 @@ def pmc_traffic(workload):
         return None, f
 
 
+STREAMS = 1  # concurrent batch streams per rank (--streams; RankGroups)
+
+
 def setup_run(name, world, rank, local_rank, exchange=True):
     """Operators, sinograms, precisions and the bound node batches of rank ``rank`` of a
     ``world``-rank run of workload ``name``.  ``exchange=False``: no inter-rank exchange (a
@@ -273,7 +276,7 @@ def setup_run(name, world, rank, local_rank, exchange=True):
     sinos = dict(zip(local, make_sinograms([ops[g] for g in local], ph, 0.005, seed=1000 + local[0])))
     Wi, Q = make_precisions(ops)  # one W kernel launch: every node shares the geometry
     rg = RankGroups(ops, G, V_total, world, rank, sinos, Q, RHO, LAM, 10 * LAM, TV_ITERS, CG_ITERS, tv_kind, ph,
-                    keep_x=True, halo=exchange)
+                    keep_x=True, halo=exchange, streams=STREAMS)
     return dict(name=name, n_img=n_img, V_total=V_total, dtype=dtype, tv_kind=tv_kind, geom=geom, plan=rg.plan,
                 rg=rg, nb=rg.batches[0], Wi=Wi, graph=cfg["graph"])
 
@@ -541,6 +544,7 @@ def leg(name, world, rank, local_rank, steps, warmup):
 
 
 def main():
+    global STREAMS
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -561,11 +565,15 @@ def main():
                     help="one GPU only: per-rank proxies of the multi-GPU runs (fast: C3 on 2, C4 on 2/4/8 "
                          "ranks; all: + C5 on 8 ranks, which also times C5 on one GPU)")
     ap.add_argument("--proxy-steps", type=int, default=3)
+    ap.add_argument("--streams", type=int, default=STREAMS,
+                    help="split each rank's nodes into up to this many batches (>= 8 float32 / 4 float64 "
+                         "nodes each) whose kernels run concurrently on their own streams")
     ap.add_argument("--headline-only", action="store_true",
                     help="only the headline workload (no weak8, strong or proxy legs): rocprofv3 runs")
     args = ap.parse_args()
     if args.headline_only:
         args.strong, args.proxy = "none", "none"
+    STREAMS = max(1, args.streams)
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
     if args.as_rank is not None and args.config is None:
@@ -647,6 +655,7 @@ def main():
             "image": n_img, "nodes": V_total, "angles_per_node": geom.n_angles,
             "graph": r["graph"],
             "parallelism": f"graph-node shards x{world}",
+            "batch_streams": len(r["rg"].streams) if r["rg"].streams else 1,
         },
         "roofline": roof,
     }

@@ -20,7 +20,7 @@ ADMM_TV_ANISO = 1
 ADMM_FUSE_MIDPOINT = 0
 ADMM_FUSE_WEIGHTED = 1
 ADMM_BATCH_KEEP_X = 1  # admm_batch.flags: x_ext local rows written only by admm_node_update
-ABI_VERSION = 6
+ABI_VERSION = 7
 ADMM_MASK_KNN = 0
 ADMM_MASK_MST = 1
 ADMM_MASK_CHAIN = 2
@@ -85,6 +85,7 @@ class Batch(C.Structure):
         ("flags", C.c_int32),
         ("y_b", C.c_void_p),
         ("w", C.c_void_p),
+        ("x_prev", C.c_void_p),
     ]
 
 

@@ -87,7 +87,7 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
              cg_iters=5, tv_kind="iso", group=None, return_tensors=False, timing=None,
              write_params=True, fusion="midpoint", inner_tol=None, max_inner_updates=10,
              inner_chunks=None, chunk_snapshot_dir=None, chunk_save_every=1, inspect=None,
-             pipeline=None):
+             pipeline=None, streams=1):
     """``inner_chunks``: split each x-update into warm-started solves of these round counts
     (block_6_admm_loop.py:14-69 chunked SCS); ``chunk_snapshot_dir`` then receives that
     file's per-chunk snapshots (``_chunk_snapshot``) every ``chunk_save_every`` chunks.
@@ -95,7 +95,8 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
     (tests check the edge invariants on the device arrays).  ``pipeline``: read the
     statistics back once after the loop instead of every iteration (default: whenever the
     stop test cannot fire and no per-iteration host output is requested; False forces the
-    per-iteration read-back).  In the pipelined mode the device keeps the statistics of at most
+    per-iteration read-back).  ``streams``: concurrent node batches per rank (groups.RankGroups;
+    bitwise the same run).  In the pipelined mode the device keeps the statistics of at most
     ``PIPELINE_BLOCK`` iterations (V_total x 8 + E x 3 float64 each) and flushes them to the host
     every ``PIPELINE_BLOCK`` iterations, so the verbose progress lines of those iterations are
     printed at each flush (and at the end), not as each iteration finishes."""
@@ -126,7 +127,7 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
         snapshot_every = max(1, max_iters // snapshot_div)  # _ver2:31-32
     rg = RankGroups(A_dense_list, G, V_total, world, rank, sinograms, Qij_diag_fn, rho, lam_tv, mu,
                     tv_iters, cg_iters, tv_kind, phantom_true, fusion=fusion, Wi_list=Wi_list,
-                    keep_x=inner_tol is None, group=group)  # this loop never writes x itself
+                    keep_x=inner_tol is None, group=group, streams=streams)  # this loop never writes x itself
     # (masked re-solves of the tolerance mode restore x rows, so that mode re-projects x)
     plan = rg.plan
     if world > 1:

@@ -35,6 +35,11 @@ def operator_key(A):
     return (A.geom, A.dtype, A.device)
 
 
+# smallest batch a concurrent split makes: a full node-interleave vector (8 float32 / 4 float64
+# nodes; admm_tomo.hip vb_for) -- narrower batches pay the per-tap address VALU per fewer nodes
+SPLIT_MIN = {"float32": 8, "float64": 4}
+
+
 def max_batch_nodes(geom) -> int:
     """Most nodes one device batch may hold: the library addresses a batch's node-interleaved
     sample buffers with 32-bit offsets (admm_batch_bind: V x max(n, m) x 8 bytes < 2^31), so
@@ -47,9 +52,14 @@ def max_batch_nodes(geom) -> int:
 class RankGroups:
     def __init__(self, A_list, G, V_total: int, world: int, rank: int, sinograms, Qij_diag_fn,
                  rho, lam, mu, tv_iters, cg_iters, tv_kind, phantom, fusion="midpoint", Wi_list=None,
-                 keep_x=False, group=None, halo=True):
+                 keep_x=False, group=None, halo=True, streams=1):
         """``halo=False``: no inter-rank exchange (bench.py's per-rank proxy: one rank's share
-        of a ``world``-rank run on one GPU, its halo rows held fixed)."""
+        of a ``world``-rank run on one GPU, its halo rows held fixed).  ``streams`` > 1: every
+        operator group of at least 2 x SPLIT_MIN nodes is split into up to that many near-equal
+        batches whose x-updates (and edge updates) run concurrently on their own HIP streams,
+        so one batch's kernels fill the other's dependent-launch gaps and kernel tails; each
+        batch keeps a full node-interleave width (SPLIT_MIN nodes), and the run is bitwise the
+        one-batch run (the batch split never changes a node's arithmetic)."""
         self.plan: ShardPlan = make_plan(G, V_total, world, rank)
         if not self.plan.local_nodes:
             raise ValueError(f"rank {rank} owns no graph nodes ({V_total} nodes over {world} ranks)")
@@ -76,6 +86,18 @@ class RankGroups:
                 split.append((k, c0))
                 members[(k, c0)] = nodes[c0:c0 + cap]
         keys = split
+        if streams > 1:  # concurrent batches: near-equal consecutive parts of >= SPLIT_MIN nodes
+            split = []
+            for k in keys:
+                nodes = members.pop(k)
+                parts = max(1, min(streams, len(nodes) // SPLIT_MIN[k[0][1]]))
+                c0 = 0
+                for q in range(parts):
+                    sz = len(nodes) // parts + (1 if q < len(nodes) % parts else 0)
+                    split.append((k, q))
+                    members[(k, q)] = nodes[c0:c0 + sz]
+                    c0 += sz
+            keys = split
         devices = {k[0][2] for k in keys}
         if len(devices) > 1:
             raise ValueError("a rank's operators must all live on one device (got "
@@ -104,6 +126,25 @@ class RankGroups:
             self.moves = [(nb, lt([row[g] for g in nb.plan.local_nodes]), lt([row[g] for g in nb.plan.halo_nodes]))
                           for nb in self.batches]
         self.halo = HaloExchange(self.plan, self.x_rank, group) if halo else None
+        # one stream per batch when several run concurrently (streams > 1)
+        self.streams = ([torch.cuda.Stream(device=self.device) for _ in self.batches]
+                        if streams > 1 and len(self.batches) > 1 else None)
+
+    def _concurrent(self, fn) -> None:
+        """fn(nb) for every batch: in order on the current stream, or (streams > 1) each on its
+        own stream, forked from and joined back into the current one."""
+        if self.streams is None:
+            for nb in self.batches:
+                fn(nb)
+            return
+        cur = torch.cuda.current_stream(self.device)
+        fork = cur.record_event()
+        for nb, s in zip(self.batches, self.streams):
+            s.wait_event(fork)
+            with torch.cuda.stream(s):
+                fn(nb)
+        for s in self.streams:
+            cur.wait_stream(s)
 
     @property
     def single(self) -> bool:
@@ -114,8 +155,7 @@ class RankGroups:
         return self.plan.V
 
     def node_update(self, rounds: int | None = None) -> None:
-        for nb in self.batches:
-            nb.node_update(rounds)
+        self._concurrent(lambda nb: nb.node_update(rounds))
 
     def exchange(self) -> None:
         """Every batch's halo rows <- the current images of their nodes (other batches of
@@ -129,8 +169,7 @@ class RankGroups:
                 torch.index_select(self.x_rank, 0, hal, out=nb.x_ext[nb.V:])
 
     def consensus(self) -> None:
-        for nb in self.batches:
-            nb.consensus()
+        self._concurrent(lambda nb: nb.consensus())
 
     def stats(self, extra=None):
         """Global node / edge statistics; ``extra`` (rank-local [V, k] numpy, rows in

@@ -43,7 +43,11 @@ class NodeBatch:
     def __init__(self, geom: ParallelBeamGeometry, dtype: str, plan: ShardPlan, sinograms,
                  Qij_diag_fn, rho: float, lam: float, mu: float, tv_iters: int = 10,
                  cg_iters: int = 5, tv_kind: str = "iso", phantom=None, device: int = 0,
-                 fusion: str = "midpoint", Wi_list=None, keep_x: bool = False):
+                 fusion: str = "midpoint", Wi_list=None, keep_x: bool = False, derive_z: bool | None = None):
+        """``derive_z`` (default: midpoint fusion): z_ij is not stored but derived from the
+        endpoint images of the last consensus (``x_prev``, one row per x_ext row; ABI 7) --
+        bitwise the same z.  block_5's drop-in, which injects arbitrary targets v_ij through z,
+        keeps it stored (``derive_z=False``)."""
         self.lib = _lib.load()
         self.geom = geom
         self.plan = plan
@@ -100,10 +104,17 @@ class NodeBatch:
         self.edge_a = ii(plan.edge_a_row)
         self.edge_b = ii(plan.edge_b_row)
         self.y = torch.zeros((max(E, 1), n), dtype=torch.float64, device=dev)
-        self.z = torch.zeros((max(E, 1), n), dtype=torch.float64, device=dev)
         # weighted edge fusion: both endpoint duals + W of every x_ext row
         if fusion not in ("midpoint", "weighted"):
             raise ValueError("fusion must be 'midpoint' or 'weighted'")
+        if derive_z is None:
+            derive_z = fusion == "midpoint"
+        if derive_z and fusion != "midpoint":
+            raise ValueError("derived z needs midpoint fusion")
+        self.derive_z = bool(derive_z)
+        # derived: x_ext at the last consensus (x = 0 before the first: z = 0); stored: z per edge
+        self.z = None if self.derive_z else torch.zeros((max(E, 1), n), dtype=torch.float64, device=dev)
+        self.x_prev = torch.zeros((plan.n_xext, n), dtype=torch.float64, device=dev) if self.derive_z else None
         self.fusion = fusion
         self.y_b = None
         self.w = None
@@ -133,11 +144,18 @@ class NodeBatch:
             p(self.edge_stats),
             _lib.ADMM_FUSE_WEIGHTED if fusion == "weighted" else _lib.ADMM_FUSE_MIDPOINT,
             _lib.ADMM_BATCH_KEEP_X if keep_x else 0,
-            p(self.y_b), p(self.w))
+            p(self.y_b), p(self.w), p(self.x_prev))
         torch.cuda.synchronize(dev)
         _lib.check(self.lib.admm_batch_bind(self.ctx.h, C.byref(self.cb)), "admm_batch_bind")
         _lib.check(self.lib.admm_batch_atb(self.ctx.h, p(self.atb), C.c_void_p(self._s())),
                    "admm_batch_atb")
+
+    def z_of(self, k: int) -> torch.Tensor:
+        """z of stored edge slot k: the stored vector, or (derived) the midpoint of its endpoint
+        rows of x_prev -- the value every kernel forms."""
+        if self.z is not None:
+            return self.z[k]
+        return (self.x_prev[self.plan.edge_a_row[k]] + self.x_prev[self.plan.edge_b_row[k]]) * 0.5
 
     def _s(self) -> int:
         return current_stream_handle(self.dev)

@@ -82,7 +82,8 @@ class _Problem:
         qs = self.q
         qfn = lambda i, j: qs[j - 1]  # noqa: E731
         nb = NodeBatch(self.A.geom, self.A.dtype, _star_plan(deg), [self.b], qfn, self.rho,
-                       self.lam, mu, tv_iters, cg_iters, tv_kind, None, self.A.device)
+                       self.lam, mu, tv_iters, cg_iters, tv_kind, None, self.A.device,
+                       derive_z=False)  # the targets v_ij are the caller's: stored as z, y = 0
         for e, v in enumerate(self.v):
             nb.z[e].copy_(torch.as_tensor(np.asarray(v) if not isinstance(v, torch.Tensor) else v)
                           .reshape(-1).to(device=nb.dev, dtype=torch.float64))

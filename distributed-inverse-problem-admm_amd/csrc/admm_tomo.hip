@@ -291,6 +291,25 @@ int with_vb(int vb, F&& f) {
   }
 }
 
+// The bound batch's forward plan and its segment-partial buffer, set together: the clipped
+// plans (3-5) write only the (segment, ray) partials of rays crossing the segment inside the
+// image and k_fwd_combine reads every slot, so whenever the plan (or the batch) changes, every
+// slot is zeroed here -- the one place C->fpart's plan is chosen (the operator API's op_fpart
+// keeps its own plan key, op_forward_chunk).
+int bind_fwd_plan(admm_ctx* C, int V) {
+  RET(with_vb(C->vb, [&](auto vbc) {
+    constexpr int VB = decltype(vbc)::value;
+    return C->dtype == ADMM_DTYPE_F32 ? choose_fwd_plan<float, VB>(C, V) : choose_fwd_plan<double, VB>(C, V);
+  }));
+  if (C->n_groups > 0) {
+    const size_t Vp = (size_t)((V + C->vb - 1) / C->vb) * C->vb;
+    RET(ensure(C->fpart, (size_t)kFgSeg * Vp * C->mrays * dsize(C->dtype)));
+    HIPCHK(hipMemset(C->fpart.p, 0, C->fpart.bytes));
+    HIPCHK(hipDeviceSynchronize());
+  }
+  return ADMM_OK;
+}
+
 template <typename T, int VB, int MODE>
 int launch_fwd(admm_ctx* C, const T* img, const T* imgT, T* sino, const T* b, double* part, int V, hipStream_t s) {
   if (C->csr) {  // explicit matrix: one thread per sinogram row
@@ -391,6 +410,18 @@ int launch_reduce(const double* part, int rows, int P, double* out, int G, int o
   return ADMM_OK;
 }
 
+// the edge state the x-update reads (stored z, or z derived from x_prev: ABI 7)
+EdgeIn edge_in(const admm_batch& B) {
+  EdgeIn E{};
+  E.z = B.z;
+  E.y = B.y;
+  E.yb = B.fusion == ADMM_FUSE_WEIGHTED ? B.y_b : nullptr;
+  E.xp = B.x_prev;
+  E.ea = B.edge_a;
+  E.eb = B.edge_b;
+  return E;
+}
+
 // --------------------------------------------------------------------------
 // the x-update sequence for the bound batch (replaces block_6_admm_loop_ver2.py:81-197)
 // --------------------------------------------------------------------------
@@ -417,16 +448,14 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 
   if (reuse) {
     // 1-4. one kernel from the previous update's A^T (A xs - b) (ADMM_BATCH_KEEP_X):
     //      c, r = A^T b + rho c + mu K^T(d - e) - H x, p = r (+ transpose)
-    hipLaunchKernelGGL((k_start_reuse<T, VB>), cgg, dim3(kBlock), 0, s, (const T*)C->ats.p, B.x_ext, B.y, B.z,
-                       B.q, B.inc_off, B.inc_edge, B.inc_qslot, B.inc_sign,
-                       B.fusion == ADMM_FUSE_WEIGHTED ? B.y_b : nullptr, B.atb, c, B.dsum, B.d, B.e, r, p, pT,
+    hipLaunchKernelGGL((k_start_reuse<T, VB>), cgg, dim3(kBlock), 0, s, (const T*)C->ats.p, B.x_ext, edge_in(B),
+                       B.q, B.inc_off, B.inc_edge, B.inc_qslot, B.inc_sign, B.atb, c, B.dsum, B.d, B.e, r, p, pT,
                        B.rho, B.mu, N, V);
     CHECK_LAUNCH();
   } else {
   // 1. neighbour gather: c = sum_j q_ij (z_ij - y_ij,i); xs = (T) x (+ transpose)
-  hipLaunchKernelGGL((k_gather<T, VB>), tg, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.q, B.inc_off, B.inc_edge,
-                     B.inc_qslot, B.inc_sign, B.fusion == ADMM_FUSE_WEIGHTED ? B.y_b : nullptr, c, xs, xsT,
-                     N, V);
+  hipLaunchKernelGGL((k_gather<T, VB>), tg, dim3(kBlock), 0, s, B.x_ext, edge_in(B), B.q, B.inc_off, B.inc_edge,
+                     B.inc_qslot, B.inc_sign, c, xs, xsT, N, V);
   CHECK_LAUNCH();
   // 2-4. r = A^T b + rho c + mu K^T(d - e) - H x,  p = r,  rr
   RET((launch_fwd_batch<T, VB, 0>(C, xs, xsT, sino, nullptr, nullptr, V, s)));
@@ -551,14 +580,12 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 
     a.cvec = c;
     a.x = B.x_ext;
     a.phantom = B.phantom;
-    a.yv = B.y;
-    a.zv = B.z;
+    a.edges = edge_in(B);
     a.qv = B.q;
     a.inc_off = B.inc_off;
     a.inc_edge = B.inc_edge;
     a.inc_qslot = B.inc_qslot;
     a.inc_sign = B.inc_sign;
-    a.ybv = B.fusion == ADMM_FUSE_WEIGHTED ? B.y_b : nullptr;
     a.rho = B.rho;
     a.lam = B.lam;
     a.mu = B.mu;
@@ -577,10 +604,42 @@ int enqueue_update_any(admm_ctx* C, hipStream_t s, bool reuse = false, int round
   return with_vb(C->vb, [&](auto vbc) { return enqueue_update<T, decltype(vbc)::value>(C, s, reuse, rounds); });
 }
 
+// rows of the derived consensus' LDS tile (0: more x_ext rows than any tile: direct kernel)
+int cons_rows(int n_xext) { return n_xext <= 16 ? 16 : n_xext <= 64 ? 64 : n_xext <= 128 ? 128 : 0; }
+
 int enqueue_consensus(admm_ctx* C, hipStream_t s) {
   const admm_batch& B = C->b;
   if (B.n_edges == 0) return ADMM_OK;
   const int npix = C->npix;
+  if (B.z == nullptr) {  // derived z (midpoint fusion, ABI 7)
+    const dim3 g((npix + kConsPix - 1) / kConsPix);
+    double* part = (double*)C->partE.p;
+    switch (cons_rows(B.n_xext)) {
+      case 16:
+        hipLaunchKernelGGL(k_consensus_derived<16>, g, dim3(kBlock), 0, s, B.x_ext, B.x_prev, B.y, B.edge_a,
+                           B.edge_b, part, npix, B.n_xext, B.n_edges);
+        break;
+      case 64:
+        hipLaunchKernelGGL(k_consensus_derived<64>, g, dim3(kBlock), 0, s, B.x_ext, B.x_prev, B.y, B.edge_a,
+                           B.edge_b, part, npix, B.n_xext, B.n_edges);
+        break;
+      case 128:
+        hipLaunchKernelGGL(k_consensus_derived<128>, g, dim3(kBlock), 0, s, B.x_ext, B.x_prev, B.y, B.edge_a,
+                           B.edge_b, part, npix, B.n_xext, B.n_edges);
+        break;
+      default: {
+        hipLaunchKernelGGL(k_consensus_derived_direct, g, dim3(kBlock), 0, s, B.x_ext, B.x_prev, B.y, B.edge_a,
+                           B.edge_b, part, npix, B.n_edges);
+        CHECK_LAUNCH();
+        const size_t cnt = (size_t)B.n_xext * npix;
+        hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)std::min<size_t>((cnt + kBlock - 1) / kBlock, 16384)),
+                           dim3(kBlock), 0, s, (const double*)B.x_ext, B.x_prev, cnt);
+      }
+    }
+    CHECK_LAUNCH();
+    RET(launch_reduce(part, 3 * B.n_edges, C->P_edge, B.edge_stats, 1, 1, 0, s));
+    return ADMM_OK;
+  }
   dim3 grid((npix + kBlock * 4 - 1) / (kBlock * 4), B.n_edges);
   if (B.fusion == ADMM_FUSE_WEIGHTED)
     hipLaunchKernelGGL(k_consensus<true>, grid, dim3(kBlock), 0, s, B.x_ext, B.y, B.y_b, B.z, B.w, B.edge_a,
@@ -1143,9 +1202,13 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   if (!(B.mu > 0)) return fail(ADMM_E_INVALID, "mu must be > 0");
   if (!B.x_ext || !B.d || !B.e || !B.atb || !B.dsum || !B.b || !B.inc_off || !B.node_stats)
     return fail(ADMM_E_INVALID, "null batch pointer");
-  if (B.n_edges > 0 && (!B.y || !B.z || !B.q || !B.edge_a || !B.edge_b || !B.inc_edge || !B.inc_qslot ||
+  if (B.n_edges > 0 && (!B.y || !B.q || !B.edge_a || !B.edge_b || !B.inc_edge || !B.inc_qslot ||
                         !B.inc_sign || !B.edge_stats))
     return fail(ADMM_E_INVALID, "null edge pointer");
+  if (B.n_edges > 0 && !B.z) {
+    if (!B.x_prev) return fail(ADMM_E_INVALID, "z == NULL needs x_prev (derived consensus)");
+    if (B.fusion != ADMM_FUSE_MIDPOINT) return fail(ADMM_E_INVALID, "derived z needs midpoint fusion");
+  }
   if (B.fusion != ADMM_FUSE_MIDPOINT && B.fusion != ADMM_FUSE_WEIGHTED) return fail(ADMM_E_INVALID, "bad fusion");
   if (B.flags & ~ADMM_BATCH_KEEP_X) return fail(ADMM_E_INVALID, "unknown batch flags");
   if (B.fusion == ADMM_FUSE_WEIGHTED && B.n_edges > 0 && (!B.y_b || !B.w))
@@ -1160,10 +1223,7 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   C->b = B;
   const int V = B.V;
   C->vb = vb_for(V, C->dtype);
-  RET(with_vb(C->vb, [&](auto vbc) {
-    constexpr int VB = decltype(vbc)::value;
-    return C->dtype == ADMM_DTYPE_F32 ? choose_fwd_plan<float, VB>(C, V) : choose_fwd_plan<double, VB>(C, V);
-  }));
+  RET(bind_fwd_plan(C, V));
   const size_t Vp = (size_t)((V + C->vb - 1) / C->vb) * C->vb;  // padded to whole chunks
   const size_t ds = dsize(C->dtype);
   RET(ensure(C->xs, Vp * npix * ds));
@@ -1180,13 +1240,6 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   C->ats_valid = false;
   RET(ensure(C->sino, Vp * m * ds));
   RET(ensure(C->bI, Vp * m * ds));
-  if (C->n_groups > 0) {
-    RET(ensure(C->fpart, (size_t)kFgSeg * Vp * m * ds));
-    // the plan writes only the (segment, ray) partials of rays crossing the segment inside
-    // the image; every other slot must read as 0 in k_fwd_combine
-    HIPCHK(hipMemset(C->fpart.p, 0, C->fpart.bytes));
-    HIPCHK(hipDeviceSynchronize());
-  }
   RET(ensure(C->r, V * npix * 8));
   RET(ensure(C->c, V * npix * 8));
   RET(ensure(C->d2, 2 * V * npix * 8));
@@ -1198,7 +1251,7 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
     return fail(ADMM_E_INVALID, "batch too large for 32-bit buffer offsets");
   C->P_fwd = (C->n_groups > 0 || C->csr) ? (int)((m + kBlock - 1) / kBlock)
                                          : ((C->g.n_det + kFwdRays - 1) / kFwdRays) * C->g.n_angles;
-  C->P_edge = (int)((npix + kBlock * 4 - 1) / (kBlock * 4));
+  C->P_edge = B.z ? (int)((npix + kBlock * 4 - 1) / (kBlock * 4)) : (int)((npix + kConsPix - 1) / kConsPix);
   RET(ensure(C->partH, (size_t)5 * V * C->P_back * 8));
   RET(ensure(C->partS, (size_t)V * C->P_fwd * 8));
   RET(ensure(C->partD, (size_t)5 * V * C->P_back * 8));

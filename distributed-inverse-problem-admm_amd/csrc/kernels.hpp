@@ -564,7 +564,11 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   // keeping 2-3 chunks in flight, measured slower)
   constexpr int R = kDma ? ADMM_FG_DMA_ROWS : kFgRows;
   constexpr int PIECES = NPL * R * 2 * kFgPieces;  // 1-KiB LDS-DMA pieces per chunk
-  __shared__ Pack<T, PV> win[kDma ? 2 : 1][NPL][R][kFgRow];
+  // two NAMED chunk buffers (not one [2][...] array): the LDS-DMA into one and the tap reads of
+  // the other then have distinct underlying objects, so the compiler's LDS-DMA alias tracking
+  // does not put a vmcnt(0) -- a wait for the next chunk's DMA -- in front of the taps
+  __shared__ Pack<T, PV> win[NPL][R][kFgRow];
+  __shared__ Pack<T, PV> win1[kDma ? NPL : 1][kDma ? R : 1][kDma ? kFgRow : 1];
   // every row window of the segment (N <= 4096): origin and the width actually touched
   __shared__ __align__(16) int wlo_s[(4096 + kFgSeg - 1) / kFgSeg + 4];  // +4: int4 reads of the last chunk
   __shared__ int wnum_s[(4096 + kFgSeg - 1) / kFgSeg + 4];
@@ -758,9 +762,13 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         // the row's touched width are fetched but never read by a tap: masking them cost more
         // VALU than the L2 fetch it saved)
         const unsigned voff = (unsigned)((col * VB + pl * PV) * (int)sizeof(T));
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rs, (__attribute__((address_space(3))) void*)&win[b][pl][r][(par ? kFgOdd : 0) + 64 * h], 16, voff,
-            0, 0, 0);
+        const int slot = (par ? kFgOdd : 0) + 64 * h;
+        if (b == 0)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)&win[pl][r][slot],
+                                                   16, voff, 0, 0, 0);
+        else
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)&win1[pl][r][slot],
+                                                   16, voff, 0, 0, 0);
       }
     };
     dma(m_lo, 0);
@@ -775,10 +783,17 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       if (m0 + R < m_hi) dma(m0 + R, cb ^ 1);
       origins(m0, wl_cur);
       const int rows = idle ? 0 : min(R, m_hi - m0);
-      if (rows == R)
-        taps4(win[cb], m0);
-      else
-        taps(win[cb], m0, rows, wl_cur);
+      if constexpr (cb == 0) {
+        if (rows == R)
+          taps4(win, m0);
+        else
+          taps(win, m0, rows, wl_cur);
+      } else {
+        if (rows == R)
+          taps4(win1, m0);
+        else
+          taps(win1, m0, rows, wl_cur);
+      }
       __syncthreads();  // this chunk's readers done; next chunk's DMA landed (vmcnt(0) + barrier)
     };
     for (int m0 = m_lo; m0 < m_hi; m0 += 2 * R) {
@@ -815,7 +830,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         if (q < R * kFgWin * NPL) {
           const int pl = q % NPL, rw = q / NPL;
           const int r = rw / kFgWin, w = rw - r * kFgWin;
-          win[0][pl][r][(w & 1) ? kFgOdd + (w >> 1) : (w >> 1)] = stage[e];
+          win[pl][r][(w & 1) ? kFgOdd + (w >> 1) : (w >> 1)] = stage[e];
         }
       }
     };
@@ -830,7 +845,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       __builtin_amdgcn_s_setprio(1);
       if (m0 + R < m_hi) fetch(m0 + R);
       __builtin_amdgcn_s_setprio(0);
-      taps(win[0], m0, idle ? 0 : min(R, m_hi - m0), wl);
+      taps(win, m0, idle ? 0 : min(R, m_hi - m0), wl);
     }
   }
   if (g < G && rl < nkq) {
@@ -903,6 +918,19 @@ __global__ __launch_bounds__(kBlock) void k_fwd_combine(const T* __restrict__ pa
 //                sum_j rho/2 q_ij (x - v_ij)^2, |x - phantom|^2   (block_6_ver2.py:135-149),
 //                |A^T s + rho (D x - c) + mu K^T e|^2 (split-Bregman stationarity residual)
 // ===========================================================================
+// Edge state a node's x-update reads (admm_batch): the duals and z, stored (z != null) or
+// derived (z == null, ABI 7): z_ij = (x_prev[a] + x_prev[b]) / 2 from the endpoint images of
+// the last consensus -- bitwise the z that consensus formed, since it computed (x_a + x_b) * 0.5
+// from the very rows it then copied into x_prev.
+struct EdgeIn {
+  const double* z;   // [E][n] stored z, or null
+  const double* y;   // [E][n] dual of the lower endpoint
+  const double* yb;  // [E][n] dual of the higher endpoint (weighted fusion) or null
+  const double* xp;  // [n_xext][n] x_prev (derived z)
+  const int* ea;     // [E] x_ext rows of the endpoints
+  const int* eb;
+};
+
 enum BackMode { BACK_PLAIN = 0, BACK_ATB = 1, BACK_WSQ = 2, BACK_H = 3, BACK_INIT = 4, BACK_DIAG = 5 };
 
 template <typename T>
@@ -933,24 +961,24 @@ struct BackArgs {
   const double* evar;       // INIT, DIAG: e [V][2][n]
   const double* x;          // DIAG: x rows of x_ext
   const double* phantom;    // DIAG (may be null)
-  const double* yv;         // DIAG: edge y [E][n]
-  const double* zv;         // DIAG: edge z [E][n]
+  EdgeIn edges;             // DIAG: edge state (y, z or x_prev, y_b)
   const double* qv;         // DIAG: q slots
   const int* inc_off;       // DIAG
   const int* inc_edge;
   const int* inc_qslot;
   const int* inc_sign;
-  const double* ybv;        // DIAG: higher-endpoint duals (weighted fusion) or null
   double rho, lam, mu;
   int tv_kind;
 };
 
-// v_ij = z_ij - y_ij,i seen from the node at incidence sign s (+1 lower endpoint):
-// single-y form y_ij,max = -y when yb is null, else the stored higher-endpoint dual.
-__device__ __forceinline__ double edge_v(const double* __restrict__ z, const double* __restrict__ y,
-                                         const double* __restrict__ yb, int s, size_t eo) {
-  if (yb == nullptr) return z[eo] - (double)s * y[eo];
-  return z[eo] - (s > 0 ? y[eo] : yb[eo]);
+// v_ij = z_ij - y_ij,i seen from the node at incidence sign s (+1 lower endpoint) for edge slot
+// e at pixel pix: single-y form y_ij,max = -y when yb is null, else the stored higher-endpoint dual.
+__device__ __forceinline__ double edge_v(const EdgeIn& E, int e, int s, int npix, int pix) {
+  const size_t eo = (size_t)e * npix + pix;
+  const double z = E.z ? E.z[eo]
+                       : (E.xp[(size_t)E.ea[e] * npix + pix] + E.xp[(size_t)E.eb[e] * npix + pix]) * 0.5;
+  if (E.yb == nullptr) return z - (double)s * E.y[eo];
+  return z - (s > 0 ? E.y[eo] : E.yb[eo]);
 }
 
 // forward difference at (i,j) of a float64 image (zero at the last row / column)
@@ -1177,8 +1205,7 @@ __device__ __forceinline__ void diag_epilogue_tile(const BackArgs<T>& A, double*
     const double rsb = sm + A.mu * kte;
     double quad = 0.0;
     for (int q = A.inc_off[v]; q < A.inc_off[v + 1]; ++q) {
-      const size_t eo = (size_t)A.inc_edge[q] * npix + pix;
-      const double vij = edge_v(A.zv, A.yv, A.ybv, A.inc_sign[q], eo);
+      const double vij = edge_v(A.edges, A.inc_edge[q], A.inc_sign[q], npix, pix);
       const double dd = xc - vij;
       quad += A.qv[(size_t)A.inc_qslot[q] * npix + pix] * dd * dd;
     }
@@ -1228,7 +1255,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
   constexpr int ANGC = (MODE == BACK_DIAG && ANGC_ > ANGC_DIAG) ? ANGC_DIAG : ANGC_;
   static_assert(ANGC % 4 == 0, "angle chunks are read as int4 groups");
   __shared__ Pack<T, PV> win[NPL][(MODE == BACK_WSQ) ? 1 : ANGC][kBWin];
-  __shared__ int4 kmin_s[2][ANGC / 4];  // per angle: window byte offset koff (see tap)
+  __shared__ int4 kmin_s[2][ANGC / 4 + 1];  // per angle: window byte offset koff (see tap); + a spare slot
   T acc[VB];
 #pragma unroll
   for (int u = 0; u < VB; ++u) acc[u] = T(0);
@@ -1296,15 +1323,27 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
                                                                      MODE == BACK_PLAIN || MODE == BACK_ATB);
   constexpr int SPER = (ANGC * kBWin * NPL + kBkThreads - 1) / kBkThreads;
   Pack<T, PV> wst[SPER];
-  auto kmin_chunk = [&](int t0, int buf) {
-    const int nt = min(ANGC, n_ang - t0);
-    if ((int)threadIdx.x < nt) {
-      const BackAngleC g = A.angc[t0 + threadIdx.x];
-      auto kf = [&](int ii, int jj) { return fma((double)ii - c0, g.Bi, fma((double)jj - c0, g.Bj, Kc)); };
-      const double kmn = fmin(fmin(kf(ib, jb), kf(ib, jhi)), fmin(kf(ihi, jb), kf(ihi, jhi)));
-      reinterpret_cast<int*>(kmin_s[buf])[threadIdx.x] = ((int)threadIdx.x * kBWin - ((int)floor(kmn) - 1)) * PB;
-    }
+  // a chunk's window offsets from its angle records; the record load (kmin_load) is split from
+  // the offset computation (kmin_store) so the PF pipeline issues it a chunk ahead, under the
+  // taps, instead of exposing its latency between the chunk-end barriers (one block per CU at
+  // 512^2: nothing else on the CU would cover it)
+  auto kmin_load = [&](int t0) {  // every thread loads (index clamped): no select, no zero-fill
+    const BackAngleC& g = A.angc[min(t0 + (int)threadIdx.x, n_ang - 1)];
+    return make_double2(g.Bi, g.Bj);
   };
+  auto kmin_store = [&](int t0, int buf, double2 bij) {
+    // the record is consumed by every thread (only the store is masked): its load is then
+    // complete on every path, and the next chunk's load into the same registers needs no
+    // vmcnt(0) -- which would also wait for the window prefetch issued before it
+    auto kf = [&](int ii, int jj) { return fma((double)ii - c0, bij.x, fma((double)jj - c0, bij.y, Kc)); };
+    const double kmn = fmin(fmin(kf(ib, jb), kf(ib, jhi)), fmin(kf(ihi, jb), kf(ihi, jhi)));
+    const int koff = ((int)threadIdx.x * kBWin - ((int)floor(kmn) - 1)) * PB;
+    // unmasked store (threads past the chunk's angles write slots no tap reads, or the spare
+    // one): a masked store lets the compiler sink the whole computation under the mask
+    reinterpret_cast<int*>(kmin_s[buf])[min((int)threadIdx.x, ANGC)] = koff;
+    (void)t0;
+  };
+  auto kmin_chunk = [&](int t0, int buf) { kmin_store(t0, buf, kmin_load(t0)); };
   auto wfetch = [&](int t0, int buf) {
     const int nt = min(ANGC, n_ang - t0);
 #pragma unroll
@@ -1359,7 +1398,11 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
   for (int t0 = 0, ci = 0; !CSR && t0 < n_ang; t0 += ANGC, ++ci) {
     const int nt = min(ANGC, n_ang - t0);
     const int kb = (PF) ? (ci & 1) : 0;  // kmin buffer of this chunk
+    double2 rec2;  // (PF) angle records of the chunk after next, loaded under this chunk's taps
     if constexpr (PF) {
+      // (the record load first: a wait the compiler places before it then covers only older,
+      // already consumed loads, not the window prefetch issued after it)
+      rec2 = kmin_load(min(t0 + 2 * ANGC, n_ang - 1));
       if (t0 + ANGC < n_ang) wfetch(t0 + ANGC, kb ^ 1);  // in flight during this chunk's taps
     } else if constexpr (MODE != BACK_WSQ) {
       __syncthreads();
@@ -1404,7 +1447,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
       if (t0 + ANGC < n_ang) {
         __syncthreads();  // this chunk's taps are done with win and kmin_s[kb]
         wcommit(t0 + ANGC);
-        if (t0 + 2 * ANGC < n_ang) kmin_chunk(t0 + 2 * ANGC, kb);
+        kmin_store(t0 + 2 * ANGC, kb, rec2);  // (garbage past the last chunk: never read)
         __syncthreads();
       }
     }
@@ -1496,10 +1539,9 @@ __device__ __forceinline__ void tile_store_T(TileT<T, VB>& tl, T* __restrict__ o
 // VB nodes of the chunk; a block is kTile x kCgRows pixels (the CG update's grid).
 template <typename T, int VB>
 __global__ __launch_bounds__(kBlock) void k_start_reuse(
-    const T* __restrict__ ats, const double* __restrict__ x, const double* __restrict__ y,
-    const double* __restrict__ z, const double* __restrict__ q, const int* __restrict__ inc_off,
-    const int* __restrict__ inc_edge, const int* __restrict__ inc_qslot, const int* __restrict__ inc_sign,
-    const double* __restrict__ yb, const double* __restrict__ atb, double* __restrict__ cvec,
+    const T* __restrict__ ats, const double* __restrict__ x, EdgeIn E, const double* __restrict__ q,
+    const int* __restrict__ inc_off, const int* __restrict__ inc_edge, const int* __restrict__ inc_qslot,
+    const int* __restrict__ inc_sign, const double* __restrict__ atb, double* __restrict__ cvec,
     const double* __restrict__ dsum, const double* __restrict__ dvar, const double* __restrict__ evar,
     double* __restrict__ r, T* __restrict__ p, T* __restrict__ pT, double rho, double mu, int N, int V) {
   constexpr int ROWS = kBlock / kTile;
@@ -1523,8 +1565,7 @@ __global__ __launch_bounds__(kBlock) void k_start_reuse(
         const double* xv = x + vo;
         double cc = 0.0;
         for (int qq = inc_off[v]; qq < inc_off[v + 1]; ++qq) {
-          const size_t eo = (size_t)inc_edge[qq] * npix + pix;
-          const double vij = edge_v(z, y, yb, inc_sign[qq], eo);
+          const double vij = edge_v(E, inc_edge[qq], inc_sign[qq], npix, pix);
           cc += q[(size_t)inc_qslot[qq] * npix + pix] * vij;
         }
         cvec[vo + pix] = cc;
@@ -1557,12 +1598,11 @@ __global__ __launch_bounds__(kBlock) void k_start_reuse(
 // gather (prologue of the x-update, block_6_admm_loop_ver2.py:85-95,137-140):
 //   c_v = sum_{e in inc(v)} q_e (z_e - sign * y_e);  xs = (T) x, xsT = xs^T
 template <typename T, int VB>
-__global__ __launch_bounds__(kBlock) void k_gather(const double* __restrict__ x, const double* __restrict__ y,
-                                                   const double* __restrict__ z, const double* __restrict__ q,
+__global__ __launch_bounds__(kBlock) void k_gather(const double* __restrict__ x, EdgeIn E,
+                                                   const double* __restrict__ q,
                                                    const int* __restrict__ inc_off, const int* __restrict__ inc_edge,
                                                    const int* __restrict__ inc_qslot,
-                                                   const int* __restrict__ inc_sign,
-                                                   const double* __restrict__ yb, double* __restrict__ c,
+                                                   const int* __restrict__ inc_sign, double* __restrict__ c,
                                                    T* __restrict__ xs, T* __restrict__ xsT, int N, int V) {
   __shared__ TileT<T, VB> tl;
   const EwMap<VB> mp;
@@ -1580,8 +1620,7 @@ __global__ __launch_bounds__(kBlock) void k_gather(const double* __restrict__ x,
       if (live) {
         double acc = 0.0;
         for (int qq = e0; qq < e1; ++qq) {
-          const size_t eo = (size_t)inc_edge[qq] * npix + pix;
-          const double vij = edge_v(z, y, yb, inc_sign[qq], eo);
+          const double vij = edge_v(E, inc_edge[qq], inc_sign[qq], npix, pix);
           acc += q[(size_t)inc_qslot[qq] * npix + pix] * vij;
         }
         c[(size_t)v * npix + pix] = acc;
@@ -2006,6 +2045,119 @@ __global__ __launch_bounds__(kBlock) void k_consensus(const double* __restrict__
 #pragma unroll
     for (int q = 0; q < 3; ++q) part[((size_t)e * 3 + q) * P + blockIdx.x] = acc[q];
   }
+}
+
+// Derived consensus (midpoint fusion, z never stored; admm_batch.x_prev, ABI 7):
+//   z' = (x_a + x_b) * 0.5,  z = (xp_a + xp_b) * 0.5  (the previous consensus' z, bit for bit),
+//   y' = y + x_a - z',  partials |x_a - z'|^2, |x_b - z'|^2, |z' - z|^2;  then x_prev = x_ext.
+// Pixel-major: a block owns 64 pixels (one per lane) and stages every x_ext and x_prev row of
+// them in LDS once; its 4 waves then take every 4th stored edge, so per edge only the dual y
+// streams through HBM (16 B per pixel, against 48 B for the stored-z kernel's x_a, x_b, y, z
+// reads and y, z writes), and the endpoint rows come from LDS however many edges share them
+// (a dense graph's 476 edges per rank touch 64 rows).  Loads of KU edges' y are issued before
+// their arithmetic.  Partials per (edge, 64-pixel block), wave-reduced in a fixed order.
+// RMAX: LDS rows (x_ext rows <= RMAX); more rows take k_consensus_derived_direct.
+constexpr int kConsPix = 64;
+template <int RMAX>
+__global__ __launch_bounds__(kBlock) void k_consensus_derived(const double* __restrict__ xext,
+                                                              double* __restrict__ xprev, double* __restrict__ y,
+                                                              const int* __restrict__ ea, const int* __restrict__ eb,
+                                                              double* __restrict__ part, int npix, int R, int E) {
+  __shared__ double xn[RMAX][kConsPix], xo[RMAX][kConsPix];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int p0 = blockIdx.x * kConsPix;
+  const int pix = p0 + lane;
+  const bool in = pix < npix;
+  for (int q = threadIdx.x; q < R * kConsPix; q += kBlock) {
+    const int r = q / kConsPix, l = q % kConsPix;
+    const int px = p0 + l;
+    double a = 0.0, b = 0.0;
+    if (px < npix) {
+      a = xext[(size_t)r * npix + px];
+      b = xprev[(size_t)r * npix + px];
+    }
+    xn[r][l] = a;
+    xo[r][l] = b;
+  }
+  __syncthreads();
+  // the old rows are in LDS: x_prev takes this iteration's images now
+  for (int q = threadIdx.x; q < R * kConsPix; q += kBlock) {
+    const int r = q / kConsPix, l = q % kConsPix;
+    if (p0 + l < npix) xprev[(size_t)r * npix + p0 + l] = xn[r][l];
+  }
+  const int P = gridDim.x;
+  constexpr int KU = 4;  // edges per wave whose y loads are in flight together
+  for (int e0 = w; e0 < E; e0 += 4 * KU) {
+    double yv[KU];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const int e = e0 + 4 * u;
+      yv[u] = (in && e < E) ? y[(size_t)e * npix + pix] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const int e = e0 + 4 * u;
+      if (e >= E) break;  // wave-uniform
+      const int a = ea[e], b = eb[e];
+      double s[3] = {0.0, 0.0, 0.0};
+      if (in) {
+        const double xa = xn[a][lane], xb = xn[b][lane];
+        const double zn = (xa + xb) * 0.5;
+        const double zo = (xo[a][lane] + xo[b][lane]) * 0.5;
+        y[(size_t)e * npix + pix] = yv[u] + xa - zn;
+        const double ra = xa - zn, rb = xb - zn, dz = zn - zo;
+        s[0] = ra * ra;
+        s[1] = rb * rb;
+        s[2] = dz * dz;
+      }
+#pragma unroll
+      for (int q = 0; q < 3; ++q) s[q] = wave_sum_d(s[q]);
+      if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) part[((size_t)e * 3 + q) * P + blockIdx.x] = s[q];
+      }
+    }
+  }
+}
+
+// The same for batches with more x_ext rows than the LDS tile holds: endpoint rows read from
+// HBM / L2 per edge (same arithmetic, same partial layout, bitwise the same results); x_prev
+// is copied by a separate pass after it (k_copy_rows) because other blocks still read it.
+__global__ __launch_bounds__(kBlock) void k_consensus_derived_direct(const double* __restrict__ xext,
+                                                                     const double* __restrict__ xprev,
+                                                                     double* __restrict__ y, const int* __restrict__ ea,
+                                                                     const int* __restrict__ eb,
+                                                                     double* __restrict__ part, int npix, int E) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int pix = blockIdx.x * kConsPix + lane;
+  const bool in = pix < npix;
+  const int P = gridDim.x;
+  for (int e = w; e < E; e += 4) {
+    const int a = ea[e], b = eb[e];
+    double s[3] = {0.0, 0.0, 0.0};
+    if (in) {
+      const double xa = xext[(size_t)a * npix + pix], xb = xext[(size_t)b * npix + pix];
+      const double zn = (xa + xb) * 0.5;
+      const double zo = (xprev[(size_t)a * npix + pix] + xprev[(size_t)b * npix + pix]) * 0.5;
+      const size_t eo = (size_t)e * npix + pix;
+      y[eo] = y[eo] + xa - zn;
+      const double ra = xa - zn, rb = xb - zn, dz = zn - zo;
+      s[0] = ra * ra;
+      s[1] = rb * rb;
+      s[2] = dz * dz;
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) s[q] = wave_sum_d(s[q]);
+    if (lane == 0) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) part[((size_t)e * 3 + q) * P + blockIdx.x] = s[q];
+    }
+  }
+}
+
+__global__ void k_copy_rows(const double* __restrict__ src, double* __restrict__ dst, size_t count) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
 }
 
 // rows of P partials -> one value each, fixed order (deterministic).

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ADMM_ABI_VERSION 6
+#define ADMM_ABI_VERSION 7
 
 #define ADMM_OK 0
 #define ADMM_E_INVALID (-1)
@@ -119,7 +119,8 @@ typedef struct admm_batch {
     const double* phantom;/* [n] or NULL  for ||x - phantom||^2                     */
 
     double* y;            /* [E][n] dual of the lower-numbered endpoint (y_ij,min)  */
-    double* z;            /* [E][n] consensus z_ij                                  */
+    double* z;            /* [E][n] consensus z_ij; NULL (ABI 7, midpoint fusion): derived
+                           * from x_prev below instead of stored                       */
     const double* q;      /* [Qslots][n] precision vectors                         */
     const int32_t* edge_a;    /* [E] x_ext row of the lower endpoint               */
     const int32_t* edge_b;    /* [E] x_ext row of the higher endpoint              */
@@ -137,6 +138,15 @@ typedef struct admm_batch {
     int32_t flags;        /* ADMM_BATCH_* (0 in ABI-2 callers that predate it: was reserved) */
     double* y_b;          /* [E][n] dual of the higher-numbered endpoint (y_ij,max)   */
     const double* w;      /* [n_xext][n] W of the node in each x_ext row (W_i, make_precisions) */
+
+    /* ABI 7: derived consensus (midpoint fusion, z == NULL).  z_ij is never stored: by the
+     * single-y invariant it is the midpoint of the two endpoint images of the last consensus
+     * (block_6_admm_loop_ver2.py:210-223 with y_ij,i + y_ij,j = 0), so the library keeps
+     * those images instead -- one row per x_ext row, not one per edge -- and forms
+     * z_ij = (x_prev[a] + x_prev[b]) / 2 wherever z is read (neighbour gather, diagnostics,
+     * the dual residual); admm_consensus sets x_prev = x_ext after its edge updates.
+     * Zero-filled by the caller before the first iteration (z = 0, block_6_..._ver2.py:42). */
+    double* x_prev;       /* [n_xext][n] or NULL (stored z)                            */
 } admm_batch;
 
 int admm_abi_version(void);

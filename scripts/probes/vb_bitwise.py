@@ -57,12 +57,12 @@ yz = {e: (torch.as_tensor(0.001 * rng.standard_normal(N * N), device="cuda"),
 res2 = {}
 for V in (1, 2, 3, 4):
     P = make_subset_plan(G, 6, range(V))
-    nb = NodeBatch(ops[0].geom, "float32", P, sinos, Q, 2.0, 0.02, 0.2, 10, 5, "iso", ph, 0)
+    nb = NodeBatch(ops[0].geom, "float32", P, sinos, Q, 2.0, 0.02, 0.2, 10, 5, "iso", ph, 0, derive_z=False)
     for r, g in enumerate(P.local_nodes + P.halo_nodes):
         nb.x_ext[r].copy_(xs_all[g])
     for s, ge in enumerate(P.stored_edges):
         nb.y[s].copy_(yz[P.edges[ge]][0])
-        nb.z[s].copy_(yz[P.edges[ge]][1])
+        nb.z[s].copy_(yz[P.edges[ge]][1])  # (stored z: derive_z=False)
     nb.node_update()
     nb.consensus()
     torch.cuda.synchronize()

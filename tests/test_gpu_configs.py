@@ -138,3 +138,28 @@ def test_large_x_updates_match_operator_oracle(cuda, monkeypatch, N, V, dtype, t
                                       eps_pri=0.0, eps_dual=0.0, phantom_true=ph, tv_kind=tv,
                                       tv_iters=tvi)
     check(x, h, xo, ho, tol)
+
+
+@pytest.mark.timeout(900)
+def test_c5_share_full_inner_count_matches_operator_oracle(cuda):
+    """C5's arithmetic at its real inner count: 2048^2, the 8-node
+    complete graph of C5's per-GPU share (C5s), float64 samples, anisotropic TV, split-Bregman
+    10 x 5, 2 ADMM iterations -- whole histories (every per-node key the reference records,
+    block_6_admm_loop_ver2.py:310-326) and images against the operator-level oracle at 1e-9.
+    The product path runs z derived from the endpoint images (ABI 7), the oracle the
+    reference's literal (a_a + a_b) / 2 -- equal to rounding."""
+    N, V = 2048, 8
+    ops, ph, sinos, Wi, Q = problem(N, V, 96, "float64")
+    G = nx.complete_graph(V)
+    x, h = gpu_run(ops, sinos, G, Wi, Q, N, 2, ph, tv_kind="aniso", tv_iters=10, cg_iters=5)
+    sin_h = [s.double().cpu().numpy() for s in sinos]
+    xo, ho = oadmm.decentralized_admm(ops, sin_h, G, Q, N, lam_tv=0.02, rho=2.0, max_iters=2,
+                                      eps_pri=0.0, eps_dual=0.0, phantom_true=ph, tv_kind="aniso",
+                                      tv_iters=10, cg_iters=5)
+    check(x, h, xo, ho, 1e-9)
+    for k in ("obj_per_node", "mse_sino_per_node", "img_mse_per_node", "pri_per_node", "dual_per_node"):
+        e = rel(np.stack(h[k]), np.stack(ho[k]))
+        print(k, f"{e:.2e}")
+        assert e < 1e-9, (k, e)
+    for k in range(V):
+        assert rel(x[k], xo[k]) < 1e-9, k

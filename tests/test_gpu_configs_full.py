@@ -10,7 +10,7 @@
   GPU (8 nodes each, the all-gather halo at the graph's real degree) bitwise equal to 1.
 * C5 -- 2048^2, 64-node complete graph (2016 edges), float64 samples, anisotropic TV,
   10 x 5, 1 ADMM iteration.  On one GPU the 64 nodes are two device batches (a batch holds
-  at most 63 nodes at this size: groups.max_batch_nodes), the 2016 edges' y / z take
+  at most 56 nodes at this size: groups.max_batch_nodes), the 2016 edges' y / z take
   ~165 GB.  Checked by properties -- after the first iteration (y = z = 0 before it)
   z = (x_a + x_b) / 2 and y = x_a - z hold exactly on every stored edge, the per-node
   statistics are finite and every image moved towards the phantom -- and 2 gloo ranks on
@@ -82,7 +82,7 @@ def _edge_check(first_iter):
             for k in range(len(nb.plan.stored_edges)):
                 xa, xb = nb.x_ext[nb.plan.edge_a_row[k]], nb.x_ext[nb.plan.edge_b_row[k]]
                 mid = (xa + xb) * 0.5
-                z, y = nb.z[k], nb.y[k]
+                z, y = nb.z_of(k), nb.y[k]
                 worst = max(worst, float(torch.linalg.norm(z - mid) / torch.linalg.norm(mid)))
                 if first_iter:
                     exact_bad += int(not torch.equal(z, mid)) + int(not torch.equal(y, xa - z))
@@ -186,7 +186,7 @@ def test_c4_ranks_match_one_rank_bitwise(cuda, world):
 def test_c5_full_graph_one_gpu_and_two_ranks(cuda):
     r1 = _spawn("C5", 1, 800)[0]
     chk = r1["chk"]
-    assert chk["batches"] == 2  # 56 + 8 nodes: one batch holds at most 63 at 2048^2
+    assert chk["batches"] == 2  # 56 + 8 nodes: one batch holds at most 56 at 2048^2
     assert chk["stored_edges"] == 1988 + 476  # edges held by both batches are stored twice
     assert chk["exact_bad"] == 0 and chk["worst"] == 0.0, chk
     h = r1["hist"]

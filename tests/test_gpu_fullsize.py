@@ -49,7 +49,7 @@ def test_fullsize_invariants_and_descent(problem):
     nb, plan, stats = run(problem, 2)
     x = nb.x_ext
     for k, (a, b) in enumerate(plan.edges):
-        z = nb.z[k]
+        z = nb.z_of(k)
         assert torch.allclose(z, 0.5 * (x[a] + x[b]), rtol=0, atol=1e-12 * float(x.abs().max()))
     ops, ph, sinos, Wi, Q = problem
     # objective at x=0 is 0.5||b||^2 (neighbour terms vanish at z=y=0) -> first update descends
