@@ -94,8 +94,8 @@ class RankGroups:
                 c0 = 0
                 for q in range(parts):
                     sz = len(nodes) // parts + (1 if q < len(nodes) % parts else 0)
-                    split.append((k, q))
-                    members[(k, q)] = nodes[c0:c0 + sz]
+                    split.append((k[0], (k[1], q)))  # (operator key, batch tag)
+                    members[(k[0], (k[1], q))] = nodes[c0:c0 + sz]
                     c0 += sz
             keys = split
         devices = {k[0][2] for k in keys}

@@ -138,6 +138,10 @@ struct admm_ctx {
   bool bound = false;
   admm_batch b{};
   int vb = 1;  // node interleave width of the sample buffers
+  // mirror mode (kernels.hpp k_fwdg MIRROR): the bound batch projects virtual images over the
+  // first half of the angles with the half geometry's context `half` (tables and plans)
+  bool mm = false;
+  admm_ctx* half = nullptr;
   Buf xs, xsT, p, pT, Hp, sino, bI, fpart, r, c, d2, e2;
   Buf dsumS;  // D = sum_j q_ij as interleaved samples (BACK_H epilogue)
   Buf x2, p2; // ping-pong partners of x (local rows) and p for the fused TV update
@@ -296,12 +300,56 @@ int with_vb(int vb, F&& f) {
 // image and k_fwd_combine reads every slot, so whenever the plan (or the batch) changes, every
 // slot is zeroed here -- the one place C->fpart's plan is chosen (the operator API's op_fpart
 // keeps its own plan key, op_forward_chunk).
+// Virtual node-interleave width of mirror mode for a real width VBR: twice VBR, at most one
+// 32-byte vector (8 float32 / 4 float64 lanes)
+template <typename T, int VBR>
+constexpr int mirror_vb() {
+  return 2 * VBR < 32 / (int)sizeof(T) ? 2 * VBR : 32 / (int)sizeof(T);
+}
+// Mirror mode applies to the geometry, not the batch (so every node runs the same arithmetic
+// whatever its batch's size: rank- and batch-invariant results): an even number of angles
+// spanning [0, pi) (block_2_load_odl_data.py:51) and a detector symmetric about 0
+// (block_2:52, uniform_partition(-1, 1, N)).  ADMM_FWD_MIRROR=1 switches it on (A/B).
+bool mirror_eligible(const admm_ctx* C) {
+  if (C->csr || C->g.n_angles < 2 || C->g.n_angles % 2 != 0) return false;
+  const char* e = getenv("ADMM_FWD_MIRROR");
+  if (!(e && e[0] == '1')) return false;  // (opt-in until measured)
+  const double pi = 3.14159265358979323846;
+  return std::fabs(C->g.angle_min) <= 1e-15 && std::fabs(C->g.angle_max - pi) <= 1e-12 &&
+         std::fabs(C->g.det_min + C->g.det_max) <= 1e-12 * std::fabs(C->g.det_max);
+}
+
 int bind_fwd_plan(admm_ctx* C, int V) {
-  RET(with_vb(C->vb, [&](auto vbc) {
-    constexpr int VB = decltype(vbc)::value;
-    return C->dtype == ADMM_DTYPE_F32 ? choose_fwd_plan<float, VB>(C, V) : choose_fwd_plan<double, VB>(C, V);
-  }));
+  C->mm = C->n_groups > 0 && mirror_eligible(C);
+  if (C->mm && !C->half) {
+    // the half geometry: the first a/2 angles, bitwise the full geometry's (angle_max - angle_min
+    // is halved exactly and so is the angle count: the same step (t + 1/2) pi / a)
+    admm_geom hg = C->g;
+    hg.n_angles = C->g.n_angles / 2;
+    hg.angle_max = C->g.angle_min + 0.5 * (C->g.angle_max - C->g.angle_min);
+    RET(admm_ctx_create(&C->half, &hg, C->dtype, 1, C->device));  // (tables and plans only)
+    if (C->half->n_groups == 0) C->mm = false;  // (cannot happen: half the angles fit as well)
+  }
+  if (C->mm) {
+    RET(with_vb(C->vb, [&](auto vbc) -> int {
+      constexpr int VBR = decltype(vbc)::value;
+      const int nchv = ((V + VBR - 1) / VBR) * (2 * VBR / (C->dtype == ADMM_DTYPE_F32 ? mirror_vb<float, VBR>()
+                                                                                      : mirror_vb<double, VBR>()));
+      if (C->dtype == ADMM_DTYPE_F32) {
+        constexpr int VBV = mirror_vb<float, VBR>();
+        return choose_fwd_plan<float, VBV>(C->half, nchv * VBV);
+      }
+      constexpr int VBV = mirror_vb<double, VBR>();
+      return choose_fwd_plan<double, VBV>(C->half, nchv * VBV);
+    }));
+  } else {
+    RET(with_vb(C->vb, [&](auto vbc) {
+      constexpr int VB = decltype(vbc)::value;
+      return C->dtype == ADMM_DTYPE_F32 ? choose_fwd_plan<float, VB>(C, V) : choose_fwd_plan<double, VB>(C, V);
+    }));
+  }
   if (C->n_groups > 0) {
+    // (mirror: virtual chunks x half the rays x the virtual width -- the same element count)
     const size_t Vp = (size_t)((V + C->vb - 1) / C->vb) * C->vb;
     RET(ensure(C->fpart, (size_t)kFgSeg * Vp * C->mrays * dsize(C->dtype)));
     HIPCHK(hipMemset(C->fpart.p, 0, C->fpart.bytes));
@@ -339,6 +387,17 @@ int launch_fwdg_taps_with(admm_ctx* C, const T* img, const T* imgT, T* fpart, co
 
 template <typename T, int VB>
 int launch_fwdg_taps(admm_ctx* C, const T* img, const T* imgT, int V, hipStream_t s) {
+  if (C->mm) {  // mirror mode: virtual chunks of the half geometry (k_fwdg MIRROR)
+    constexpr int VBV = mirror_vb<T, VB>(), MH = VBV / 2;
+    const int nchv = ((V + VB - 1) / VB) * (VB / MH);
+    const admm_ctx* H = C->half;
+    if (nchv != H->fg_order_nch) return fail(ADMM_E_STATE, "mirror block table built for another batch size");
+    hipLaunchKernelGGL((k_fwdg<T, VBV, true, VB>), dim3(H->fg_nblk), dim3(kFgThreads), 0, s, img, imgT,
+                       (T*)C->fpart.p, H->fang, H->groups, H->rng, (const int4*)H->fg_order.p, C->g.N, C->g.n_det,
+                       H->g.n_angles, nchv * VBV);
+    CHECK_LAUNCH();
+    return ADMM_OK;
+  }
   const int nch = (V + VB - 1) / VB;
   if (nch != C->fg_order_nch) return fail(ADMM_E_STATE, "forward block table built for another batch size");
   return launch_fwdg_taps_with<T, VB>(C, img, imgT, (T*)C->fpart.p, C->groups, C->rng,
@@ -363,6 +422,15 @@ int launch_fwd_batch(admm_ctx* C, const T* img, const T* imgT, T* sino, const T*
   const int nch = (V + VB - 1) / VB;
   RET((launch_fwdg_taps<T, VB>(C, img, imgT, V, s)));
   if (ev) HIPCHK(hipEventRecord(ev[1], s));
+  if (C->mm) {  // virtual partials -> the real sinogram (both angles of every virtual ray)
+    constexpr int VBV = mirror_vb<T, VB>(), MH = VBV / 2;
+    const int mh = C->half->mrays;
+    dim3 mg((mh + kBlock - 1) / kBlock, nch * (VB / MH));
+    hipLaunchKernelGGL((k_fwd_combine_mirror<T, VBV, VB, MODE>), mg, dim3(kBlock), 0, s, (const T*)C->fpart.p, sino,
+                       b, part, C->half->fang, C->g.n_det, C->half->g.n_angles, V);
+    CHECK_LAUNCH();
+    return ADMM_OK;
+  }
   dim3 cg((C->mrays + kBlock - 1) / kBlock, nch);
   hipLaunchKernelGGL((k_fwd_combine<T, VB, MODE>), cg, dim3(kBlock), 0, s, (const T*)C->fpart.p, sino, b, part,
                      C->fang, C->g.n_det, C->g.n_angles, V);
@@ -1113,6 +1181,8 @@ int admm_ctx_destroy(admm_ctx* C) {
   DeviceGuard _dg(C->device);
   (void)hipDeviceSynchronize();
   free_graphs(C);
+  if (C->half) (void)admm_ctx_destroy(C->half);
+  C->half = nullptr;
   Buf* bufs[] = {&C->op_img, &C->op_imgT, &C->op_sino, &C->op_fpart, &C->xs, &C->xsT, &C->p, &C->pT, &C->Hp, &C->sino, &C->bI, &C->fpart, &C->r, &C->c,
                  &C->d2, &C->e2, &C->partH, &C->partS, &C->partD, &C->partE, &C->redH, &C->fg_order, &C->dsumS, &C->ats,
                  &C->f_ptr, &C->f_idx, &C->f_val, &C->t_ptr, &C->t_idx, &C->t_val, &C->x2, &C->p2, &C->pring};
@@ -1249,7 +1319,8 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   C->P_tile = ((N + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
   if ((size_t)Vp * npix * ds >= (1ull << 31) || (size_t)Vp * m * ds >= (1ull << 31))
     return fail(ADMM_E_INVALID, "batch too large for 32-bit buffer offsets");
-  C->P_fwd = (C->n_groups > 0 || C->csr) ? (int)((m + kBlock - 1) / kBlock)
+  C->P_fwd = C->mm ? (int)((C->half->mrays + kBlock - 1) / kBlock)
+           : (C->n_groups > 0 || C->csr) ? (int)((m + kBlock - 1) / kBlock)
                                          : ((C->g.n_det + kFwdRays - 1) / kFwdRays) * C->g.n_angles;
   C->P_edge = B.z ? (int)((npix + kBlock * 4 - 1) / (kBlock * 4)) : (int)((npix + kConsPix - 1) / kConsPix);
   RET(ensure(C->partH, (size_t)5 * V * C->P_back * 8));
@@ -1434,6 +1505,7 @@ int admm_time_forward(admm_ctx* C, int reps, int in_solve, void* stream, double*
 int admm_fwd_plan_info(admm_ctx* C, int plan, int* groups, int* blocks, double* staged, int* active) {
   if (!C || plan < 0 || plan >= admm_ctx::kPlans || !groups || !blocks || !staged || !active)
     return fail(ADMM_E_INVALID, "bad argument");
+  if (C->mm && C->half) C = C->half;  // mirror mode: the half geometry's plans are the bound ones
   *groups = C->plan_n[plan];
   *blocks = C->plan_blocks[plan];
   *staged = C->plan_staged[plan];

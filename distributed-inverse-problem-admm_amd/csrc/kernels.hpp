@@ -522,12 +522,27 @@ struct FgRange {
 #define ADMM_FG_WPE 8  // waves per SIMD the register budget must allow: <= 64 VGPRs, 2 blocks/CU
                        // (float64 samples otherwise take 67 and fall to one block per CU)
 #endif
-template <typename T, int VB>
+// MIRROR (the mirror-symmetric projection, admm_tomo.hip "mirror mode"): the geometry's angles
+// are (t + 1/2) pi / a over [0, pi) with a symmetric detector, so angle a-1-t = pi - theta_t
+// projects image I exactly as angle t projects flipud(I) (same detector order;
+// tests/test_oracle.py::test_mirror_symmetry_of_the_joseph_operator).  A batch then projects
+// VIRTUAL images over the first a/2 angles only: virtual lanes u < VB/2 are real node lanes at
+// (i, j), lanes u >= VB/2 the same real nodes at (N-1-i, j).  The virtual image is never stored:
+// staging reads the real node-interleaved buffers (VBR lanes per pixel) with the mirrored half
+// taken from row N-1-m (case B, img) or column N-1-w (case A, img^T).  A narrow batch (4 float32
+// nodes: VBR = 4) thereby projects 8-lane vectors -- the per-tap address / weight VALU is paid
+// once per 8 lanes as in an 8-node batch -- and an 8-node batch runs two virtual chunks of
+// half the angles (the same taps).  Virtual chunk c' = real chunk c' / S, lane block c' % S of
+// VB/2 real lanes (S = 2 VBR / VB).
+template <typename T, int VB, bool MIRROR = false, int VBR = VB>
 __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM_FG_WPE))) void k_fwdg(const T* __restrict__ img, const T* __restrict__ imgT,
                                                  T* __restrict__ part, const FwdAngle* __restrict__ ang,
                                                  const FgGroup* __restrict__ groups, const FgRange* __restrict__ rng,
                                                  const int4* __restrict__ order, int N, int n_det, int n_ang, int V) {
   constexpr int NPL = Planes<T, VB>::NPL, PV = Planes<T, VB>::PV;
+  constexpr int MH = VB / 2;                  // (MIRROR) real lanes per virtual chunk
+  constexpr int MS = MIRROR ? VBR / MH : 1;   // (MIRROR) virtual chunks per real chunk
+  static_assert(!MIRROR || (VB % 2 == 0 && VBR % MH == 0), "mirror: VB = 2 x (a divisor of VBR)");
   constexpr int PER = (kFgRows * kFgWin * NPL + kFgThreads - 1) / kFgThreads;  // staged packs per thread
   // g (the wave's angle slot) is wave-uniform: readfirstlane lets the compiler keep it, and
   // everything derived from it (group offsets, DMA piece indices, the idle test), in SGPRs
@@ -548,7 +563,10 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   const int kcl = clampi(k, 0, n_det - 1);
   const int t = t0 + gq;
   const FwdAngle a = ang[t];
-  const T* src = (ang[t0].caseA ? imgT : img) + (size_t)chunk * npix * VB;
+  const bool caseA = ang[t0].caseA != 0;
+  // real buffer of this (virtual) chunk; MIRROR: real chunk chunk / MS, lane block mq
+  const int mq = MIRROR ? chunk % MS : 0;
+  const T* src = (caseA ? imgT : img) + (size_t)(MIRROR ? chunk / MS : chunk) * npix * VBR;
   const double l0 = fma((double)kcl, a.A1, a.A0);
   const int m_lo = seg * N / kFgSeg, m_hi = (seg + 1) * N / kFgSeg;
   const int nrows = m_hi - m_lo;
@@ -558,7 +576,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   // hardware, scripts/probes/dma_oob.hip), two chunk buffers, one barrier per chunk, and no
   // VGPRs or ds_write instructions spent on staging.  float64 x 8 nodes (4 planes) keeps the
   // register-staged single buffer (two would not fit two blocks per CU).
-  constexpr bool kDma = sizeof(Pack<T, PV>) == 16 && NPL <= 2;
+  constexpr bool kDma = sizeof(Pack<T, PV>) == 16 && NPL <= 2 && (!MIRROR || NPL == 2);
   // rows per staged chunk (2 in the LDS-DMA kernel: the next chunk's DMA is issued a
   // 2-row chunk of taps ahead; 4-row chunks, or a 3/4-buffer ring with counted vmcnt waits
   // keeping 2-3 chunks in flight, measured slower)
@@ -740,7 +758,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   if constexpr (kDma) {
     // one 1-KiB piece per wave-instruction: 64 consecutive 16-B slots of one (plane, row,
     // parity half); a row's even half holds pixels wlo + 2s, its odd half wlo + 2s + 1
-    const uint32_t rowbytes = (uint32_t)N * VB * (uint32_t)sizeof(T);
+    const uint32_t rowbytes = (uint32_t)N * VBR * (uint32_t)sizeof(T);
     auto dma = [&](int m0, int b) {
       const int rows = min(R, m_hi - m0);
       for (int q = g; q < PIECES; q += kFgG) {  // wave-uniform
@@ -752,16 +770,20 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         if (128 * h + par >= wn) continue;  // piece wholly past the touched width
         // the row base is block-uniform: force it into SGPRs (a VGPR base makes hipcc wrap
         // the DMA in a waterfall loop over the distinct resource values)
-        const uint64_t rb = (uint64_t)(uintptr_t)(src + (size_t)(m0 + r) * N * VB);
+        // MIRROR: virtual plane 1 is the real lane block mirrored -- case B from row N-1-m
+        const int srow = (MIRROR && pl == 1 && !caseA) ? N - 1 - (m0 + r) : m0 + r;
+        const uint64_t rb = (uint64_t)(uintptr_t)(src + (size_t)srow * N * VBR);
         const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)rb);
         const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(rb >> 32));
         const __amdgpu_buffer_rsrc_t rs =
             make_rsrc((const void*)(uintptr_t)(((uint64_t)hi << 32) | lo), rowbytes);
-        const int col = wo + 128 * h + par + 2 * lane;
+        int col = wo + 128 * h + par + 2 * lane;
+        if (MIRROR && pl == 1 && caseA) col = N - 1 - col;  // case A: column N-1-w of the same row
         // negative columns wrap to huge unsigned offsets: out of range, zero-filled (slots past
         // the row's touched width are fetched but never read by a tap: masking them cost more
         // VALU than the L2 fetch it saved)
-        const unsigned voff = (unsigned)((col * VB + pl * PV) * (int)sizeof(T));
+        const unsigned voff = MIRROR ? (unsigned)((col * VBR + mq * MH) * (int)sizeof(T))
+                                     : (unsigned)((col * VB + pl * PV) * (int)sizeof(T));
         const int slot = (par ? kFgOdd : 0) + 64 * h;
         if (b == 0)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)&win[pl][r][slot],
@@ -815,7 +837,17 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         // both reads unconditional (in bounds: +4 padding), so they issue together
         const int wn = wnum_s[m0 - m_lo + r], wo = wlo_s[m0 - m_lo + r];
         const int col = (r < rows && w < wn) ? wo + w : -1;
-        if (q < R * kFgWin * NPL && col >= 0 && col < N) {
+        if constexpr (MIRROR) {  // element-wise: a virtual plane may mix the two orientations
+#pragma unroll
+          for (int z = 0; z < PV; ++z) {
+            const int u = pl * PV + z, o = u >= MH;
+            const int srow = (o && !caseA) ? N - 1 - (m0 + r) : m0 + r;
+            const int scol = (o && caseA) ? N - 1 - col : col;
+            stage[e].v[z] = (q < R * kFgWin * NPL && col >= 0 && col < N)
+                                ? src[((size_t)srow * N + scol) * VBR + mq * MH + (u - o * MH)]
+                                : T(0);
+          }
+        } else if (q < R * kFgWin * NPL && col >= 0 && col < N) {
           stage[e] = *reinterpret_cast<const Pack<T, PV>*>(src + ((size_t)(m0 + r) * N + col) * VB + pl * PV);
         } else {
 #pragma unroll
@@ -899,6 +931,69 @@ __global__ __launch_bounds__(kBlock) void k_fwd_combine(const T* __restrict__ pa
 #pragma unroll
       for (int u = 0; u < VB; ++u)
         if (u < nv) pout[(size_t)(v0 + u) * gridDim.x + blockIdx.x] = sq[u];
+    }
+  }
+}
+
+// The mirror-mode combine (k_fwdg<..., MIRROR>): virtual chunk c' of the half geometry's rays
+// (a/2 angles) -> the REAL sinogram (VBR lanes, a angles) of real chunk c' / MS, lane block
+// c' % MS: lanes u < VB/2 are angle t, lanes u >= VB/2 angle a-1-t (pi - theta_t) of the same
+// real nodes.  MODE 1: s = A x - b against the real node-major b, and per real node one
+// ||s||^2 partial per block holding both of its angles' residuals (summed in a fixed order).
+template <typename T, int VB, int VBR, int MODE>
+__global__ __launch_bounds__(kBlock) void k_fwd_combine_mirror(const T* __restrict__ part, T* __restrict__ sino,
+                                                               const T* __restrict__ bsino,
+                                                               double* __restrict__ pout,
+                                                               const FwdAngle* __restrict__ ang, int n_det,
+                                                               int n_ang_half, int V) {
+  constexpr int MH = VB / 2, MS = VBR / MH;
+  const int chunk = blockIdx.y, nch = gridDim.y;  // virtual chunks
+  const int rc = chunk / MS, mq = chunk % MS;     // real chunk, lane block
+  const int vr0 = rc * VBR + mq * MH;             // first real node of the lane block
+  const size_t m_half = (size_t)n_ang_half * n_det, m_full = 2 * m_half;
+  const size_t ray = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  double sq[MH];
+#pragma unroll
+  for (int u = 0; u < MH; ++u) sq[u] = 0.0;
+  if (ray < m_half) {
+    const int t = (int)(ray / n_det), k = (int)(ray % n_det);
+    const size_t ray2 = (size_t)(2 * n_ang_half - 1 - t) * n_det + k;  // angle a-1-t
+    const T L = (T)ang[t].L;
+    T acc[VB], pv[VB];
+    gload<T, VB>(part + ((size_t)chunk * m_half + ray) * VB, acc);
+#pragma unroll
+    for (int sg = 1; sg < kFgSeg; ++sg) {
+      gload<T, VB>(part + (((size_t)sg * nch + chunk) * m_half + ray) * VB, pv);
+#pragma unroll
+      for (int u = 0; u < VB; ++u) acc[u] += pv[u];
+    }
+    T lo[MH], hi[MH];
+#pragma unroll
+    for (int u = 0; u < MH; ++u) {
+      lo[u] = acc[u] * L;
+      hi[u] = acc[MH + u] * L;
+      if (MODE == 1) {
+        if (vr0 + u < V) {
+          lo[u] -= bsino[(size_t)(vr0 + u) * m_full + ray];
+          hi[u] -= bsino[(size_t)(vr0 + u) * m_full + ray2];
+          sq[u] = (double)lo[u] * (double)lo[u] + (double)hi[u] * (double)hi[u];
+        } else {
+          lo[u] = T(0);
+          hi[u] = T(0);
+        }
+      }
+    }
+    T* base = sino + (size_t)rc * m_full * VBR + mq * MH;  // (MH-lane blocks: aligned vector stores)
+    gstore<T, MH>(base + ray * VBR, lo);
+    gstore<T, MH>(base + ray2 * VBR, hi);
+  }
+  if (MODE == 1) {
+    __shared__ double lds[4 * MH];
+    block_reduce<MH>(sq, lds);
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int u = 0; u < MH; ++u)
+        if (vr0 + u < V) pout[(size_t)(vr0 + u) * gridDim.x + blockIdx.x] = sq[u];
     }
   }
 }
@@ -1220,8 +1315,20 @@ __device__ __forceinline__ void diag_epilogue_tile(const BackArgs<T>& A, double*
   }
 }
 
+#ifndef ADMM_BK_NARROW_WPE
+#define ADMM_BK_NARROW_WPE 1  // 8: A/B candidate (64 VGPRs, spills 10 in H mode)
+#endif
+// Waves per SIMD the register budget must allow: float samples at VB <= 4 (narrow batches:
+// C4's 4-node share per GPU at 8 GPUs) fit 64 VGPRs, so two 1024-thread blocks share a CU and
+// one block's window staging / epilogue overlaps the other's taps (the wide kernels need more
+// than 64 and run one block per CU).
+template <typename T, int VB, int MODE>
+constexpr int back_waves_per_eu() {
+  return (std::is_same<T, float>::value && VB <= 4 && (MODE == BACK_H || MODE == BACK_INIT)) ? ADMM_BK_NARROW_WPE : 1;
+}
 template <typename T, int VB, int MODE, bool CSR = false>
-__global__ __launch_bounds__(kBkThreads) void k_back(BackArgs<T> A) {
+__global__ __launch_bounds__(kBkThreads) __attribute__((amdgpu_waves_per_eu(back_waves_per_eu<T, VB, MODE>())))
+void k_back(BackArgs<T> A) {
   constexpr int NQ = (MODE == BACK_H) ? 5 : (MODE == BACK_DIAG) ? 5 : 1;
   constexpr int NPL = Planes<T, VB>::NPL, PV = Planes<T, VB>::PV;
   const int N = A.N, n_det = A.n_det, n_ang = A.n_ang;

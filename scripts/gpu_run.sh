@@ -6,6 +6,7 @@
 #   prof       rocprofv3 --kernel-trace --stats of the headline -> gpurun_out/prof_TAG
 #   bench      the default bench line (CPU baseline, weak8, strong C4, proxies fast)
 #   benchall   the default bench line with --proxy all (adds C5 on 8 ranks and C5 on one GPU)
+#   hl, hl2    headline only, no CPU baseline (--streams 1 / 2): quick A/B lines
 #   configs    bench.py --config C2 C3 C4 C5s
 #   smoke      __graft_entry__.smoke()
 # Every step has its own time limit; the first failing step ends the session.
@@ -43,6 +44,10 @@ for step in "$@"; do
     benchall)
       run benchall 900 python bench.py --steps 20 --warmup 5 --proxy all > gpurun_out/benchall_${TAG}.json 2> gpurun_out/benchall_${TAG}.err || { tail -5 gpurun_out/benchall_${TAG}.err; exit 1; }
       python scripts/summarize_bench.py gpurun_out/benchall_${TAG}.json ;;
+    hl|hl2|hl4)  # quick headline A/B (no CPU baseline): hl = default streams, hl2 / hl4 = --streams 2 / 4
+      st=1; [ "$step" = hl2 ] && st=2; [ "$step" = hl4 ] && st=4
+      run $step 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --headline-only --streams $st > gpurun_out/${step}_${TAG}.json 2> gpurun_out/${step}_${TAG}.err || { tail -5 gpurun_out/${step}_${TAG}.err; exit 1; }
+      python scripts/summarize_bench.py gpurun_out/${step}_${TAG}.json ;;
     configs)
       run configs 1000 bash scripts/run_configs.sh C2 C3 C4 C5s || exit 1 ;;
     smoke)

@@ -281,3 +281,20 @@ def test_eps_target_and_stop_rule():
                                     cg_iters=1)
     assert len(h["primal"]) == 1
     assert np.isnan(h["img_mse_total"][0])  # phantom_true=None (the reference crashes, _ver2:205)
+
+
+def test_mirror_symmetry_of_the_joseph_operator():
+    """The identity the mirror-mode forward projector rests on (kernels.hpp k_fwdg MIRROR):
+    with angles (t + 1/2) pi / a over [0, pi) and the symmetric detector of
+    block_2_load_odl_data.py:51-52, angle a-1-t (= pi - theta_t) projects image I exactly as
+    angle t projects flipud(I), bin for bin (to float64 rounding of the geometry)."""
+    import numpy as np
+    from oracle.geometry import Geometry, joseph_matrix
+    for N, a in ((32, 16), (33, 12), (40, 96)):
+        A = joseph_matrix(Geometry(N, a))
+        rng = np.random.default_rng(N)
+        X = rng.standard_normal((N, N))
+        s = (A @ X.ravel()).reshape(a, N)
+        sf = (A @ X[::-1, :].ravel()).reshape(a, N)
+        t = np.arange(a // 2)
+        assert np.abs(sf[t] - s[a - 1 - t]).max() <= 1e-12 * np.abs(s).max()
