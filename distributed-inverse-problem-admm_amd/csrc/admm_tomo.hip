@@ -440,6 +440,26 @@ int launch_fwd_batch(admm_ctx* C, const T* img, const T* imgT, T* sino, const T*
 
 template <typename T, int VB, int MODE>
 int launch_back(admm_ctx* C, BackArgs<T> a, int V, hipStream_t s) {
+  if constexpr (MODE == BACK_H || MODE == BACK_INIT || MODE == BACK_DIAG || MODE == BACK_ATB) {
+    if (C->mm) {  // mirror mode: pixel pairs of the upper half, the half geometry's angles
+      constexpr int VBV = mirror_vb<T, VB>(), MH = VBV / 2;
+      const admm_ctx* H = C->half;
+      a.ang = H->bang;
+      a.angc = H->bangc;
+      a.K = H->Kb;
+      a.kbias = H->kbias;
+      a.wexp = H->wexp;
+      a.N = C->g.N;
+      a.n_det = C->g.n_det;
+      a.n_ang = H->g.n_angles;
+      a.V = V;
+      const int N = C->g.N, Nh = (N + 1) / 2;
+      dim3 grid((N + kBTJ - 1) / kBTJ, (Nh + kBTI - 1) / kBTI, ((V + VB - 1) / VB) * (VB / MH));
+      hipLaunchKernelGGL((k_back_mirror<T, VBV, VB, MODE>), grid, dim3(kBkThreads), 0, s, a);
+      CHECK_LAUNCH();
+      return ADMM_OK;
+    }
+  }
   a.ang = C->bang;
   a.angc = C->bangc;
   a.K = C->Kb;
@@ -465,7 +485,8 @@ int launch_back(admm_ctx* C, BackArgs<T> a, int V, hipStream_t s) {
 
 int back_partitions(admm_ctx* C) {
   const int N = C->g.N;
-  return ((N + kBTJ - 1) / kBTJ) * ((N + kBTI - 1) / kBTI);
+  const int rows = C->mm ? (N + 1) / 2 : N;  // mirror mode: blocks over the upper half's pixel pairs
+  return ((N + kBTJ - 1) / kBTJ) * ((rows + kBTI - 1) / kBTI);
 }
 dim3 tile_grid(admm_ctx* C, int nchunks, int vb) {
   const int N = C->g.N, ti = kTile / vb;

@@ -1115,15 +1115,16 @@ __device__ __forceinline__ double kt_w_at(const double* __restrict__ d, const do
 
 // Fused epilogue of one pixel: writes the mode's per-pixel outputs and adds the
 // pixel's reduction terms into pq.
-template <typename T, int VB, int MODE, int NQ>
+// VS / lo (mirror mode): the VB lanes handled are lanes lo .. lo+VB-1 of VS-lane sample vectors.
+template <typename T, int VB, int MODE, int NQ, int VS = VB>
 __device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j, int chunk, int v0, int nv,
-                                              const T (&acc)[VB], double (&pq)[VB][NQ]) {
+                                              const T (&acc)[VB], double (&pq)[VB][NQ], int lo = 0) {
   const int N = A.N;
   const int npix = N * N;
   const int pix = i * N + j;
-  const size_t sbase = (size_t)chunk * npix * VB;  // interleaved sample base of this chunk
+  const size_t sbase = (size_t)chunk * npix * VS + lo;  // interleaved sample base of this chunk
   if constexpr (MODE == BACK_PLAIN) {
-    gstore<T, VB>(A.out_t + sbase + (size_t)pix * VB, acc);
+    gstore<T, VB>(A.out_t + sbase + (size_t)pix * VS, acc);
   } else if constexpr (MODE == BACK_ATB) {
 #pragma unroll
     for (int u = 0; u < VB; ++u)
@@ -1135,33 +1136,33 @@ __device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j
     const T* pv = A.pin + sbase;
     T pc[VB], pn[VB];
     double ktk[VB];
-    gload<T, VB>(pv + (size_t)pix * VB, pc);
+    gload<T, VB>(pv + (size_t)pix * VS, pc);
 #pragma unroll
     for (int u = 0; u < VB; ++u) ktk[u] = 0.0;
     if (i >= 1) {
-      gload<T, VB>(pv + (size_t)(pix - N) * VB, pn);
+      gload<T, VB>(pv + (size_t)(pix - N) * VS, pn);
 #pragma unroll
       for (int u = 0; u < VB; ++u) ktk[u] += (double)pc[u] - (double)pn[u];
     }
     if (i <= N - 2) {
-      gload<T, VB>(pv + (size_t)(pix + N) * VB, pn);
+      gload<T, VB>(pv + (size_t)(pix + N) * VS, pn);
 #pragma unroll
       for (int u = 0; u < VB; ++u) ktk[u] -= (double)pn[u] - (double)pc[u];
     }
     if (j >= 1) {
-      gload<T, VB>(pv + (size_t)(pix - 1) * VB, pn);
+      gload<T, VB>(pv + (size_t)(pix - 1) * VS, pn);
 #pragma unroll
       for (int u = 0; u < VB; ++u) ktk[u] += (double)pc[u] - (double)pn[u];
     }
     if (j <= N - 2) {
-      gload<T, VB>(pv + (size_t)(pix + 1) * VB, pn);
+      gload<T, VB>(pv + (size_t)(pix + 1) * VS, pn);
 #pragma unroll
       for (int u = 0; u < VB; ++u) ktk[u] -= (double)pn[u] - (double)pc[u];
     }
     T outv[VB], dv[VB];
     // H: D read as one sample vector (float64 D rounded to T: a 2^-24-relative change of the
     // rho D p term, far below the float32 Hp it produces); INIT keeps float64 D
-    if constexpr (MODE == BACK_H) gload<T, VB>(A.dsum_s + sbase + (size_t)pix * VB, dv);
+    if constexpr (MODE == BACK_H) gload<T, VB>(A.dsum_s + sbase + (size_t)pix * VS, dv);
 #pragma unroll
     for (int u = 0; u < VB; ++u) {
       outv[u] = T(0);
@@ -1189,7 +1190,7 @@ __device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j
         }
       }
     }
-    gstore<T, VB>(A.out_t + sbase + (size_t)pix * VB, outv);
+    gstore<T, VB>(A.out_t + sbase + (size_t)pix * VS, outv);
   }  // BACK_DIAG: diag_epilogue_tile (block-cooperative)
 }
 
@@ -1236,18 +1237,18 @@ constexpr int kBAngC = ADMM_BK_ANGC;  // angles per staged sinogram-window chunk
 // the TV subgradient of every point (tile + the halo row/column above/left) is computed
 // ONCE into LDS -- the per-pixel form evaluated it at three points and re-read x nine
 // times.  `scratch`: (kBTI+2)(kBTJ+2) + 2 (kBTI+1)(kBTJ+1) doubles of LDS.
-template <typename T, int VB>
+template <typename T, int VB, int VS = VB>
 __device__ __forceinline__ void diag_epilogue_tile(const BackArgs<T>& A, double* scratch, int ib, int jb, int i,
                                                    int j, bool inb, int chunk, int v0, int nv, const T (&acc)[VB],
-                                                   double (&pq)[VB][5]) {
+                                                   double (&pq)[VB][5], int lo = 0) {
   constexpr int XC = kBTJ + 2, XR = kBTI + 2, SC = kBTJ + 1, SR = kBTI + 1;
   double* xt = scratch;            // [XR][XC]: rows ib-1 .. ib+kBTI, cols jb-1 .. jb+kBTJ
   double* sx = xt + XR * XC;       // [SR][SC]: subgradient at rows ib-1 .. ib+kBTI-1, cols jb-1 ..
   double* sy = sx + SR * SC;
   const int N = A.N, npix = N * N;
   const int pix = i * N + j;
-  const size_t sbase = (size_t)chunk * npix * VB;
-  if (inb && A.out_t) gstore<T, VB>(A.out_t + sbase + (size_t)pix * VB, acc);
+  const size_t sbase = (size_t)chunk * npix * VS + lo;
+  if (inb && A.out_t) gstore<T, VB>(A.out_t + sbase + (size_t)pix * VS, acc);
   const int ti = i - ib + 1, tj = j - jb + 1;  // this pixel in the staged x tile
 #pragma unroll
   for (int u = 0; u < VB; ++u) {  // constant bounds keep acc / pq in registers
@@ -1593,6 +1594,239 @@ void k_back(BackArgs<T> A) {
     block_reduce_rs<NV, kBkWaves>(flat, lds, tot);
     const int t = threadIdx.x;
     if (t < VB * NQ && t / NQ < nv) {
+      const int P = gridDim.x * gridDim.y;
+      const int b = blockIdx.y * gridDim.x + blockIdx.x;
+      A.part[((size_t)v0 * NQ + t) * P + b] = tot[t];
+    }
+  }
+}
+
+// ===========================================================================
+// Mirror-mode back projector (the adjoint of k_fwdg<..., MIRROR>; admm_tomo.hip mirror mode).
+// A virtual lane block holds real nodes at (i, j) (lanes < VB/2) and at (N-1-i, j) (lanes >=
+// VB/2) over the first a/2 angles; its window bins are the real sinogram's rays (t, k) and
+// (a-1-t, k).  The real A^T s at (i, j) is the virtual result at (i, j), lanes < VB/2, plus the
+// virtual result at (N-1-i, j), lanes >= VB/2 -- so each thread takes the pixel PAIR (i, j),
+// (N-1-i, j) of an upper-half tile (i < ceil(N/2)) and both pixels' real sums form in its own
+// registers: per (pixel, angle) one address / weight computation serves VB lanes (8 float32
+// lanes even for a 4-node batch), and the fused epilogues (H, INIT, DIAG, ATB) run unchanged on
+// the real lane block of both pixels (back_epilogue / diag_epilogue_tile with VS = VBR lanes per
+// real vector).  Two LDS windows per angle (upper tile, mirror tile) at half the angles per
+// chunk keep the LDS size and the staged bytes per tap of k_back.
+// ===========================================================================
+template <typename T, int VB, int VBR, int MODE>
+__global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
+  static_assert(MODE == BACK_H || MODE == BACK_INIT || MODE == BACK_DIAG || MODE == BACK_ATB, "batch modes");
+  constexpr int MH = VB / 2, MS = VBR / MH;
+  static_assert(VB % 2 == 0 && VBR % MH == 0, "mirror: VB = 2 x (a divisor of VBR)");
+  constexpr int NQ = (MODE == BACK_H || MODE == BACK_DIAG) ? 5 : 1;
+  constexpr int NPL = Planes<T, VB>::NPL, PV = Planes<T, VB>::PV;
+  constexpr int PB = (int)sizeof(Pack<T, PV>);
+  const int N = A.N, n_det = A.n_det, n_ang = A.n_ang;  // n_ang: the half geometry's a/2 angles
+  const int Nh = (N + 1) / 2;
+  const size_t m_full = (size_t)2 * n_ang * n_det;
+  const int jb = blockIdx.x * kBTJ, ib = blockIdx.y * kBTI;  // upper tile: rows ib .. (< Nh)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int j = jb + 16 * (wv % kBkPatchJ) + (lane & 15);
+  const int i = ib + 4 * (wv / kBkPatchJ) + (lane >> 4);
+  const int i2 = N - 1 - i;                  // the mirror pixel's row
+  const bool inb = (i < Nh) && (j < N);
+  const bool inb2 = inb && (i2 != i);        // (odd N: the middle row pairs with itself)
+  const int chunk = blockIdx.z, rc = chunk / MS, mq = chunk % MS;
+  const int v0 = rc * VBR + mq * MH;         // first real node of this lane block
+  const int nv = min(MH, A.V - v0);
+  const double c0 = 0.5 * (N - 1);
+  // clamped coordinates keep out-of-tile threads inside the windows; the mirror pixel's
+  // x-coordinate is exactly -xi ((N-1-i) - c0 = c0 - i)
+  const double xi = (double)min(i, Nh - 1) - c0, yj = (double)min(j, N - 1) - c0;
+  const int jhi = min(jb + kBTJ - 1, N - 1), ihi = min(ib + kBTI - 1, Nh - 1);
+  const int kbias = A.kbias;
+  const double Kc = A.K + (double)kbias;
+  constexpr int ANGC_ = ((NPL > 2) ? kBAngC / 2 : kBAngC) / 2;
+  constexpr int ANGC_DIAG = (98304 / (2 * NPL * kBWin * PB)) & ~3;
+  constexpr int ANGC = (MODE == BACK_DIAG && ANGC_ > ANGC_DIAG) ? ANGC_DIAG : ANGC_;
+  static_assert(ANGC % 4 == 0 && ANGC >= 4, "angle chunks are read as int4 groups");
+  __shared__ Pack<T, PV> win[2][NPL][ANGC][kBWin];   // [window: upper / mirror tile]
+  __shared__ int4 kmin_s[2][2][ANGC / 4 + 1];         // [buffer][window]: byte offsets koff
+  T acc1[VB], acc2[VB];
+#pragma unroll
+  for (int u = 0; u < VB; ++u) acc1[u] = acc2[u] = T(0);
+  const T* sino_c = A.sino + (size_t)rc * m_full * VBR + mq * MH;  // the real lane block
+  int t0c = 0;
+
+  // window offsets of a chunk: per angle and window the floor of the smallest corner k_f
+  // (upper tile rows ib .. ihi, mirror tile rows N-1-ihi .. N-1-ib); the record load is split
+  // from the store so the pipeline issues it a chunk ahead (as in k_back)
+  auto kmin_load = [&](int t0) {
+    const BackAngleC& g = A.angc[min(t0 + ((int)threadIdx.x % ANGC), n_ang - 1)];
+    return make_double2(g.Bi, g.Bj);
+  };
+  auto kmin_store = [&](int buf, double2 bij) {
+    const int w = (int)threadIdx.x / ANGC;  // threads 0 .. 2 ANGC - 1: (window, angle)
+    const double xa = (double)ib - c0, xb = (double)ihi - c0;
+    const double x0 = w ? -xb : xa, x1 = w ? -xa : xb;  // the window's row range (x-coordinates)
+    auto kf = [&](double xx, int jj) { return fma(xx, bij.x, fma((double)jj - c0, bij.y, Kc)); };
+    const double kmn = fmin(fmin(kf(x0, jb), kf(x0, jhi)), fmin(kf(x1, jb), kf(x1, jhi)));
+    const int a = (int)threadIdx.x % ANGC;
+    const int koff = (a * kBWin - ((int)floor(kmn) - 1)) * PB;
+    reinterpret_cast<int*>(kmin_s[buf][min(w, 1)])[w < 2 ? a : ANGC] = koff;  // (spare slot)
+  };
+  auto kmin_chunk = [&](int t0, int buf) { kmin_store(buf, kmin_load(t0)); };
+  constexpr int NE = 2 * ANGC * kBWin * NPL;  // staged packs per chunk
+  constexpr int SPER = (NE + kBkThreads - 1) / kBkThreads;
+  Pack<T, PV> wst[SPER];
+  auto wfetch = [&](int t0, int buf) {
+    const int nt = min(ANGC, n_ang - t0);
+#pragma unroll
+    for (int e = 0; e < SPER; ++e) {
+      const int q = threadIdx.x + e * kBkThreads;
+      const int pl = q % NPL, rest = q / NPL, bin = rest % kBWin, aw = rest / kBWin;
+      const int a = aw % ANGC, w = aw / ANGC;
+      const bool live = q < NE && a < nt;
+      const int k = live ? a * kBWin - reinterpret_cast<const int*>(kmin_s[buf][w])[a] / PB + bin - kbias : -1;
+      const int t = t0 + a;
+      const size_t ray0 = (size_t)t * n_det + k, ray1 = (size_t)(2 * n_ang - 1 - t) * n_det + k;
+      if (live && k >= 0 && k < n_det) {
+        if constexpr (NPL == 2) {  // virtual plane pl = orientation pl: one 16-B real plane
+          wst[e] = *reinterpret_cast<const Pack<T, PV>*>(sino_c + (pl ? ray1 : ray0) * VBR);
+        } else {                   // one virtual plane holds both orientations: element gather
+#pragma unroll
+          for (int z = 0; z < PV; ++z) wst[e].v[z] = z < MH ? sino_c[ray0 * VBR + z] : sino_c[ray1 * VBR + z - MH];
+        }
+      } else {
+#pragma unroll
+        for (int z = 0; z < PV; ++z) wst[e].v[z] = T(0);
+      }
+    }
+  };
+  auto wcommit = [&](int t0) {
+    const int nt = min(ANGC, n_ang - t0);
+#pragma unroll
+    for (int e = 0; e < SPER; ++e) {
+      const int q = threadIdx.x + e * kBkThreads;
+      const int pl = q % NPL, rest = q / NPL, bin = rest % kBWin, aw = rest / kBWin;
+      const int a = aw % ANGC, w = aw / ANGC;
+      if (q < NE && a < nt) win[w][pl][a][bin] = wst[e];
+    }
+  };
+  // one angle's taps of one pixel from window W (k_back's tap)
+  auto tap1 = [&](auto wc_, const BackAngleC& g, double kf, int koff, int tt, T(&acc)[VB]) {
+    constexpr int w = decltype(wc_)::value;
+    {
+      const int k0 = (int)kf;  // == floor(kf): kf > 0
+      const T f = (T)__builtin_amdgcn_fract(kf);
+      T w0, w1;
+      if constexpr (std::is_same<T, float>::value) {
+        float2v wc, fv, ww;
+        asm("v_mov_b64 %0, %1" : "=v"(wc) : "s"(g.wc));
+        fv.x = f;
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] clamp" : "=v"(ww) : "v"(fv), "s"(g.ws), "v"(wc));
+        w0 = ww.x;
+        w1 = ww.y;
+      } else {
+        const BackAngle& gd = A.ang[t0c + tt];
+        w0 = fmax(T(0), T(1) - f * (T)gd.slope) * (T)gd.L;
+        w1 = fmax(T(0), T(1) - (T(1) - f) * (T)gd.slope) * (T)gd.L;
+      }
+      const int off = k0 * PB + koff;
+#pragma unroll
+      for (int q = 0; q < NPL; ++q) {
+        const char* wb = reinterpret_cast<const char*>(&win[w][q][0][0]) + off;
+        const Pack<T, PV> s0 = *reinterpret_cast<const Pack<T, PV>*>(wb);
+        const Pack<T, PV> s1 = *reinterpret_cast<const Pack<T, PV>*>(wb + PB);
+#pragma unroll
+        for (int e = 0; e < PV; ++e) {
+          acc[q * PV + e] = fma(w0, s0.v[e], acc[q * PV + e]);
+          acc[q * PV + e] = fma(w1, s1.v[e], acc[q * PV + e]);
+        }
+      }
+    }
+  };
+  // both pixels: kf at xi and at -xi (the mirror pixel), sharing the j term
+  auto tap2 = [&](const BackAngleC& g, int koff1, int koff2, int tt) {
+    const double inner = fma(yj, g.Bj, Kc);
+    tap1(std::integral_constant<int, 0>{}, g, fma(xi, g.Bi, inner), koff1, tt, acc1);
+    tap1(std::integral_constant<int, 1>{}, g, fma(-xi, g.Bi, inner), koff2, tt, acc2);
+  };
+  // register-prefetched chunk pipeline (k_back's PF path)
+  kmin_chunk(0, 0);
+  __syncthreads();
+  wfetch(0, 0);
+  wcommit(0);
+  if (ANGC < n_ang) kmin_chunk(ANGC, 1);
+  __syncthreads();
+  for (int t0 = 0, ci = 0; t0 < n_ang; t0 += ANGC, ++ci) {
+    const int nt = min(ANGC, n_ang - t0);
+    const int kb = ci & 1;
+    const double2 rec2 = kmin_load(min(t0 + 2 * ANGC, n_ang - 1));
+    if (t0 + ANGC < n_ang) wfetch(t0 + ANGC, kb ^ 1);  // in flight during this chunk's taps
+    t0c = t0;
+    int tt = 0;
+    for (; tt + 4 <= nt; tt += 4) {
+      BackAngleC g[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) g[u] = A.angc[t0 + tt + u];
+      const int4 k1 = kmin_s[kb][0][tt >> 2], k2 = kmin_s[kb][1][tt >> 2];
+      tap2(g[0], k1.x, k2.x, tt);
+      tap2(g[1], k1.y, k2.y, tt + 1);
+      tap2(g[2], k1.z, k2.z, tt + 2);
+      tap2(g[3], k1.w, k2.w, tt + 3);
+    }
+    for (; tt < nt; ++tt) {
+      const BackAngleC g = A.angc[t0 + tt];
+      tap2(g, reinterpret_cast<const int*>(kmin_s[kb][0])[tt], reinterpret_cast<const int*>(kmin_s[kb][1])[tt], tt);
+    }
+    if (t0 + ANGC < n_ang) {
+      __syncthreads();  // this chunk's taps are done with win and kmin_s[kb]
+      wcommit(t0 + ANGC);
+      kmin_store(kb, rec2);  // (garbage past the last chunk: never read)
+      __syncthreads();
+    }
+  }
+  if constexpr (std::is_same<T, float>::value) {
+    if (A.wexp != 0) {
+#pragma unroll
+      for (int u = 0; u < VB; ++u) {
+        acc1[u] = ldexpf(acc1[u], A.wexp);
+        acc2[u] = ldexpf(acc2[u], A.wexp);
+      }
+    }
+  }
+  // the real A^T s of both pixels: angles < a/2 from the pixel itself, angles >= a/2 from the
+  // mirror pixel's mirrored lanes (fixed order: first half + second half)
+  T r1[MH], r2[MH];
+#pragma unroll
+  for (int h = 0; h < MH; ++h) {
+    r1[h] = acc1[h] + acc2[MH + h];
+    r2[h] = acc2[h] + acc1[MH + h];
+  }
+  double pq[MH][NQ];
+#pragma unroll
+  for (int u = 0; u < MH; ++u)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) pq[u][q] = 0.0;
+  if constexpr (MODE == BACK_DIAG) {
+    __shared__ double diag_s[(kBTI + 2) * (kBTJ + 2) + 2 * (kBTI + 1) * (kBTJ + 1)];
+    diag_epilogue_tile<T, MH, VBR>(A, diag_s, ib, jb, i, j, inb, rc, v0, nv, r1, pq, mq * MH);
+    diag_epilogue_tile<T, MH, VBR>(A, diag_s, N - ib - kBTI, jb, i2, j, inb2, rc, v0, nv, r2, pq, mq * MH);
+  } else {
+    if (inb) back_epilogue<T, MH, MODE, NQ, VBR>(A, i, j, rc, v0, nv, r1, pq, mq * MH);
+    if (inb2) back_epilogue<T, MH, MODE, NQ, VBR>(A, i2, j, rc, v0, nv, r2, pq, mq * MH);
+  }
+  if constexpr (MODE == BACK_H || MODE == BACK_DIAG) {
+    constexpr int NV = ((MH * NQ + 15) / 16) * 16;
+    __shared__ double lds[kBkWaves * NV];
+    __shared__ double tot[NV];
+    double flat[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) flat[k] = 0.0;
+#pragma unroll
+    for (int u = 0; u < MH; ++u)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) flat[u * NQ + q] = pq[u][q];
+    block_reduce_rs<NV, kBkWaves>(flat, lds, tot);
+    const int t = threadIdx.x;
+    if (t < MH * NQ && t / NQ < nv) {
       const int P = gridDim.x * gridDim.y;
       const int b = blockIdx.y * gridDim.x + blockIdx.x;
       A.part[((size_t)v0 * NQ + t) * P + b] = tot[t];

@@ -44,10 +44,14 @@ for step in "$@"; do
     benchall)
       run benchall 900 python bench.py --steps 20 --warmup 5 --proxy all > gpurun_out/benchall_${TAG}.json 2> gpurun_out/benchall_${TAG}.err || { tail -5 gpurun_out/benchall_${TAG}.err; exit 1; }
       python scripts/summarize_bench.py gpurun_out/benchall_${TAG}.json ;;
-    hl|hl2|hl4)  # quick headline A/B (no CPU baseline): hl = default streams, hl2 / hl4 = --streams 2 / 4
-      st=1; [ "$step" = hl2 ] && st=2; [ "$step" = hl4 ] && st=4
-      run $step 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --headline-only --streams $st > gpurun_out/${step}_${TAG}.json 2> gpurun_out/${step}_${TAG}.err || { tail -5 gpurun_out/${step}_${TAG}.err; exit 1; }
+    hl|hl2|hl4|hlm|hlm2)  # quick headline A/B (no CPU baseline): --streams 1/2/4; m = ADMM_FWD_MIRROR=1
+      st=1; case $step in *2) st=2 ;; *4) st=4 ;; esac
+      mm=0; case $step in hlm*) mm=1 ;; esac
+      ADMM_FWD_MIRROR=$mm run $step 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --headline-only --streams $st > gpurun_out/${step}_${TAG}.json 2> gpurun_out/${step}_${TAG}.err || { tail -5 gpurun_out/${step}_${TAG}.err; exit 1; }
       python scripts/summarize_bench.py gpurun_out/${step}_${TAG}.json ;;
+    benchallm)  # benchall with the mirror-mode forward
+      ADMM_FWD_MIRROR=1 run benchallm 900 python bench.py --steps 20 --warmup 5 --proxy all --no-cpu-baseline > gpurun_out/benchallm_${TAG}.json 2> gpurun_out/benchallm_${TAG}.err || { tail -5 gpurun_out/benchallm_${TAG}.err; exit 1; }
+      python scripts/summarize_bench.py gpurun_out/benchallm_${TAG}.json ;;
     configs)
       run configs 1000 bash scripts/run_configs.sh C2 C3 C4 C5s || exit 1 ;;
     smoke)
