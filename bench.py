@@ -475,6 +475,8 @@ def forward_roofline(r, workload, fwd_reps):
         # the angle-group plan the batch bound (admm_fwd_plan_info): 0 = 64-ray chunks,
         # 1 = aligned per (segment, angle), 2 = aligned per (segment, chunk); 3-5 = clipped
         "fwd_plan": next((dict(p) for p in nb.fwd_plans() if p["active"]), None),
+        # mirror mode: the batch projects virtual images over half the angles (admm_batch_info)
+        "mirror": nb.mirror,
         "bound": "hbm",
         "achieved": fwd_traffic / fwd_s / 1e9 if fwd_traffic is not None else None,
         "peak": HBM_PEAK_GBS,

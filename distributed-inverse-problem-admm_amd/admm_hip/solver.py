@@ -172,6 +172,13 @@ class NodeBatch:
         return min(vb, 4) if self.dtype == "float64" else vb
 
     @property
+    def mirror(self) -> bool:
+        """The bound batch's projectors run in mirror mode (admm_batch_info, ABI 8)."""
+        vb, mm = C.c_int(), C.c_int()
+        _lib.check(self.lib.admm_batch_info(self.ctx.h, C.byref(vb), C.byref(mm)), "admm_batch_info")
+        return bool(mm.value)
+
+    @property
     def x_local(self) -> torch.Tensor:
         return self.x_ext[: self.plan.V]
 

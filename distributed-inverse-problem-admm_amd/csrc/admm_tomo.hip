@@ -1523,6 +1523,14 @@ int admm_time_forward(admm_ctx* C, int reps, int in_solve, void* stream, double*
   return ADMM_OK;
 }
 
+int admm_batch_info(admm_ctx* C, int* vb, int* mirror) {
+  if (!C || !vb || !mirror) return fail(ADMM_E_INVALID, "bad argument");
+  if (!C->bound) return fail(ADMM_E_STATE, "no batch bound");
+  *vb = C->vb;
+  *mirror = C->mm ? 1 : 0;
+  return ADMM_OK;
+}
+
 int admm_fwd_plan_info(admm_ctx* C, int plan, int* groups, int* blocks, double* staged, int* active) {
   if (!C || plan < 0 || plan >= admm_ctx::kPlans || !groups || !blocks || !staged || !active)
     return fail(ADMM_E_INVALID, "bad argument");

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ADMM_ABI_VERSION 7
+#define ADMM_ABI_VERSION 8
 
 #define ADMM_OK 0
 #define ADMM_E_INVALID (-1)
@@ -224,6 +224,13 @@ int admm_time_forward(admm_ctx* ctx, int reps, int in_solve, void* stream, doubl
  * the bound batch (or, before a bind, the context) uses.  groups = 0: no such plan.
  * No device work.  (Tests and tuning; the plans give bitwise-identical projections.) */
 int admm_fwd_plan_info(admm_ctx* ctx, int plan, int* groups, int* blocks, double* staged, int* active);
+/* ABI 8: how the bound batch projects: vb = node-interleave width of its sample buffers;
+ * mirror = 1 if the projectors run in mirror mode (angles (t + 1/2) pi / a over [0, pi), a even,
+ * symmetric detector: angle a-1-t projects I as angle t projects flipud(I), so each batch
+ * projects virtual images -- its nodes at (i, j) and at (N-1-i, j) -- over the first a/2 angles,
+ * full-width sample vectors even for narrow batches; admm_fwd_plan_info then reports the half
+ * geometry's plans).  No device work. */
+int admm_batch_info(admm_ctx* ctx, int* vb, int* mirror);
 
 /* --- per-pixel edge masks for masked precisions (setup) --- */
 

@@ -298,3 +298,21 @@ def test_mirror_symmetry_of_the_joseph_operator():
         sf = (A @ X[::-1, :].ravel()).reshape(a, N)
         t = np.arange(a // 2)
         assert np.abs(sf[t] - s[a - 1 - t]).max() <= 1e-12 * np.abs(s).max()
+
+
+def test_mirror_identity_of_the_adjoint():
+    """The mirror-mode back projector's identity (kernels.hpp k_back_mirror): with A_h the
+    first a/2 angles, A^T s = A_h^T s[:a/2] + flipud(A_h^T s_m), s_m[t] = s[a-1-t] -- the real
+    A^T s at (i, j) is the half-angle back projection at (i, j) plus the mirrored half's at
+    (N-1-i, j)."""
+    import numpy as np
+    from oracle.geometry import Geometry, joseph_matrix
+    for N, a in ((32, 16), (33, 12)):
+        A = joseph_matrix(Geometry(N, a))
+        Ah = joseph_matrix(Geometry(N, a), angles=list(range(a // 2)))
+        rng = np.random.default_rng(a)
+        s = rng.standard_normal((a, N))
+        full = (A.T @ s.ravel()).reshape(N, N)
+        first = (Ah.T @ s[: a // 2].ravel()).reshape(N, N)
+        second = (Ah.T @ s[::-1][: a // 2].ravel()).reshape(N, N)[::-1, :]
+        assert np.abs(full - (first + second)).max() <= 1e-12 * np.abs(full).max()
