@@ -386,7 +386,7 @@ def time_share(name, world, rank, steps, warmup):
     """Rank ``rank``'s share of a ``world``-rank run of ``name``, timed on this GPU."""
     import torch
     r = setup_run(name, world, rank, 0, exchange=False)
-    el = timed_steps(r, steps, warmup, 1)
+    el = timed_steps(r, steps, max(warmup, 3), 1)  # (>= 2 replays of the reuse graph before timing)
     plan, nb = r["plan"], r["nb"]
     out = {"rank": rank, "local_nodes": plan.V, "halo_rows": len(plan.halo_nodes),
            "stored_edges": len(plan.stored_edges), "batches": len(r["rg"].batches), "vb": nb.ctx_vb,
@@ -536,10 +536,10 @@ def leg(name, world, rank, local_rank, steps, warmup):
     r = setup_run(name, world, rank, local_rank)
     if world > 1:
         dist.barrier()
-    el = timed_steps(r, steps, warmup, world)
+    el = timed_steps(r, steps, max(warmup, 3), world)  # (>= 2 replays of the reuse graph before timing)
     out = {"config": name, "scaling": "strong" if name != "weak8" else "weak", "workload": describe(r, world),
            "nodes": r["V_total"], "value": r["V_total"] * steps / el, "unit": "node-updates/s",
-           "ms_per_step": 1e3 * el / steps, "steps": steps, "warmup": warmup}
+           "ms_per_step": 1e3 * el / steps, "steps": steps, "warmup": max(warmup, 3)}
     del r
     torch.cuda.empty_cache()
     return out
@@ -562,11 +562,11 @@ def main():
     ap.add_argument("--strong", default=None,
                     help="strong-scaling configs measured after the headline, comma separated "
                          "(default: C4 on one GPU, C3,C4 on N > 1; 'none' to skip)")
-    ap.add_argument("--strong-steps", type=int, default=3)
+    ap.add_argument("--strong-steps", type=int, default=5)
     ap.add_argument("--proxy", choices=("none", "fast", "all"), default="fast",
                     help="one GPU only: per-rank proxies of the multi-GPU runs (fast: C3 on 2, C4 on 2/4/8 "
                          "ranks; all: + C5 on 8 ranks, which also times C5 on one GPU)")
-    ap.add_argument("--proxy-steps", type=int, default=3)
+    ap.add_argument("--proxy-steps", type=int, default=6)
     ap.add_argument("--streams", type=int, default=STREAMS,
                     help="split each rank's nodes into up to this many batches (>= 8 float32 / 4 float64 "
                          "nodes each) whose kernels run concurrently on their own streams")

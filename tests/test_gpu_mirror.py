@@ -32,7 +32,7 @@ def _run(N, V, a_per, dtype, iters=3, graph="ring"):
     ph = shepp_logan(N)
     sinos = make_sinograms(ops, ph, 0.005, seed=1000)
     Wi, Q = make_precisions(ops)
-    G = nx.cycle_graph(V) if graph == "ring" else nx.empty_graph(V)
+    G = nx.cycle_graph(V) if graph == "ring" and V > 2 else nx.path_graph(V) if graph == "ring" else nx.empty_graph(V)
     x, h = decentralized_admm(ops, sinos, G, Wi, Q, N, lam_tv=0.02, rho=2.0, max_iters=iters, eps_pri=0.0,
                               eps_dual=0.0, verbose=False, phantom_true=ph.numpy(), write_params=False,
                               tv_iters=4, cg_iters=3)
