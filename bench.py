@@ -253,6 +253,7 @@ def pmc_traffic(workload):
 
 
 STREAMS = 1  # concurrent batch streams per rank (--streams; RankGroups)
+STORED_Z = False  # --stored-z: keep z per edge instead of deriving it (A/B of ABI 7)
 
 
 def setup_run(name, world, rank, local_rank, exchange=True):
@@ -276,7 +277,7 @@ def setup_run(name, world, rank, local_rank, exchange=True):
     sinos = dict(zip(local, make_sinograms([ops[g] for g in local], ph, 0.005, seed=1000 + local[0])))
     Wi, Q = make_precisions(ops)  # one W kernel launch: every node shares the geometry
     rg = RankGroups(ops, G, V_total, world, rank, sinos, Q, RHO, LAM, 10 * LAM, TV_ITERS, CG_ITERS, tv_kind, ph,
-                    keep_x=True, halo=exchange, streams=STREAMS)
+                    keep_x=True, halo=exchange, streams=STREAMS, derive_z=False if STORED_Z else None)
     return dict(name=name, n_img=n_img, V_total=V_total, dtype=dtype, tv_kind=tv_kind, geom=geom, plan=rg.plan,
                 rg=rg, nb=rg.batches[0], Wi=Wi, graph=cfg["graph"])
 
@@ -383,14 +384,23 @@ def busiest_rank(name, world):
 
 
 def time_share(name, world, rank, steps, warmup):
-    """Rank ``rank``'s share of a ``world``-rank run of ``name``, timed on this GPU."""
+    """Rank ``rank``'s share of a ``world``-rank run of ``name``, timed on this GPU; also the
+    edge updates alone (``consensus_ms``: consensus + statistics, event-timed)."""
     import torch
     r = setup_run(name, world, rank, 0, exchange=False)
     el = timed_steps(r, steps, max(warmup, 3), 1)  # (>= 2 replays of the reuse graph before timing)
     plan, nb = r["plan"], r["nb"]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    reps = 5
+    ev[0].record()
+    for _ in range(reps):
+        r["rg"].consensus()
+    ev[1].record()
+    torch.cuda.synchronize()
     out = {"rank": rank, "local_nodes": plan.V, "halo_rows": len(plan.halo_nodes),
            "stored_edges": len(plan.stored_edges), "batches": len(r["rg"].batches), "vb": nb.ctx_vb,
-           "ms_per_step": 1e3 * el / steps, "steps": steps,
+           "mirror": nb.mirror, "z": "stored" if nb.z is not None else "derived",
+           "ms_per_step": 1e3 * el / steps, "steps": steps, "consensus_ms": ev[0].elapsed_time(ev[1]) / reps,
            "exchange": exchange_model(plan, r["n_img"])}
     del r, nb, plan
     torch.cuda.empty_cache()
@@ -546,7 +556,7 @@ def leg(name, world, rank, local_rank, steps, warmup):
 
 
 def main():
-    global STREAMS
+    global STREAMS, STORED_Z
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -570,12 +580,15 @@ def main():
     ap.add_argument("--streams", type=int, default=STREAMS,
                     help="split each rank's nodes into up to this many batches (>= 8 float32 / 4 float64 "
                          "nodes each) whose kernels run concurrently on their own streams")
+    ap.add_argument("--stored-z", action="store_true",
+                    help="keep z per edge (the pre-ABI-7 edge state) instead of deriving it: A/B")
     ap.add_argument("--headline-only", action="store_true",
                     help="only the headline workload (no weak8, strong or proxy legs): rocprofv3 runs")
     args = ap.parse_args()
     if args.headline_only:
         args.strong, args.proxy = "none", "none"
     STREAMS = max(1, args.streams)
+    STORED_Z = bool(args.stored_z)
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
     if args.as_rank is not None and args.config is None:

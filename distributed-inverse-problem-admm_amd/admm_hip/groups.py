@@ -52,7 +52,7 @@ def max_batch_nodes(geom) -> int:
 class RankGroups:
     def __init__(self, A_list, G, V_total: int, world: int, rank: int, sinograms, Qij_diag_fn,
                  rho, lam, mu, tv_iters, cg_iters, tv_kind, phantom, fusion="midpoint", Wi_list=None,
-                 keep_x=False, group=None, halo=True, streams=1):
+                 keep_x=False, group=None, halo=True, streams=1, derive_z=None):
         """``halo=False``: no inter-rank exchange (bench.py's per-rank proxy: one rank's share
         of a ``world``-rank run on one GPU, its halo rows held fixed).  ``streams`` > 1: every
         operator group of at least 2 x SPLIT_MIN nodes is split into up to that many near-equal
@@ -112,7 +112,7 @@ class RankGroups:
             geom, dtype, device = k[0]
             self.batches.append(NodeBatch(geom, dtype, gp, sinograms, Qij_diag_fn, rho, lam, mu, tv_iters,
                                           cg_iters, tv_kind, phantom, device, fusion=fusion, Wi_list=Wi_list,
-                                          keep_x=keep_x))
+                                          keep_x=keep_x, derive_z=derive_z))
         self.device = self.batches[0].dev
         if len(self.batches) == 1:
             self.x_rank = self.batches[0].x_ext

@@ -164,19 +164,21 @@ class NodeBatch:
     def V(self) -> int:
         return self.plan.V
 
+    def _info(self) -> tuple[int, bool]:
+        vb, mm = C.c_int(), C.c_int()
+        _lib.check(self.lib.admm_batch_info(self.ctx.h, C.byref(vb), C.byref(mm)), "admm_batch_info")
+        return vb.value, bool(mm.value)
+
     @property
     def ctx_vb(self) -> int:
-        """Node-interleave width the library uses for this batch (admm_tomo.hip vb_for)."""
-        V = self.plan.V
-        vb = 8 if V >= 5 else 4 if V >= 3 else V
-        return min(vb, 4) if self.dtype == "float64" else vb
+        """Node-interleave width the library chose for this batch (admm_batch_info, ABI 8):
+        vb_for(V) in admm_tomo.hip, capped at 16-byte vectors in mirror mode."""
+        return self._info()[0]
 
     @property
     def mirror(self) -> bool:
         """The bound batch's projectors run in mirror mode (admm_batch_info, ABI 8)."""
-        vb, mm = C.c_int(), C.c_int()
-        _lib.check(self.lib.admm_batch_info(self.ctx.h, C.byref(vb), C.byref(mm)), "admm_batch_info")
-        return bool(mm.value)
+        return self._info()[1]
 
     @property
     def x_local(self) -> torch.Tensor:

@@ -295,11 +295,6 @@ int with_vb(int vb, F&& f) {
   }
 }
 
-// The bound batch's forward plan and its segment-partial buffer, set together: the clipped
-// plans (3-5) write only the (segment, ray) partials of rays crossing the segment inside the
-// image and k_fwd_combine reads every slot, so whenever the plan (or the batch) changes, every
-// slot is zeroed here -- the one place C->fpart's plan is chosen (the operator API's op_fpart
-// keeps its own plan key, op_forward_chunk).
 // Virtual node-interleave width of mirror mode for a real width VBR: twice VBR, at most one
 // 32-byte vector (8 float32 / 4 float64 lanes)
 template <typename T, int VBR>
@@ -319,8 +314,18 @@ bool mirror_eligible(const admm_ctx* C) {
          std::fabs(C->g.det_min + C->g.det_max) <= 1e-12 * std::fabs(C->g.det_max);
 }
 
+// The bound batch's forward plan and its segment-partial buffer, set together: the clipped
+// plans (3-5) write only the (segment, ray) partials of rays crossing the segment inside the
+// image and k_fwd_combine reads every slot, so whenever the plan (or the batch) changes, every
+// slot is zeroed here -- the one place C->fpart's plan is chosen (the operator API's op_fpart
+// keeps its own plan key, op_forward_chunk).
 int bind_fwd_plan(admm_ctx* C, int V) {
   C->mm = C->n_groups > 0 && mirror_eligible(C);
+  // mirror mode keeps the real sample vectors at 16 bytes (4 float32 / 2 float64 nodes): a
+  // virtual chunk then stages every byte of the real vectors it reads -- with 32-byte real
+  // vectors each virtual chunk read every other 16 bytes and its sibling chunk the rest
+  // (C3: 76 vs 58 us per forward launch, profiles/r4_mirror_ab.txt)
+  if (C->mm) C->vb = std::min(C->vb, 16 / (int)dsize(C->dtype));
   if (C->mm && !C->half) {
     // the half geometry: the first a/2 angles, bitwise the full geometry's (angle_max - angle_min
     // is halved exactly and so is the angle count: the same step (t + 1/2) pi / a)

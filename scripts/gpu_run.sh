@@ -16,10 +16,10 @@ TAG=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 run() {  # name, limit, command...
   local name=$1 lim=$2; shift 2
-  echo "== $name"
+  echo "== $name" >&2
   timeout -k 10 $lim "$@"
   local rc=$?
-  echo "== $name rc=$rc"
+  echo "== $name rc=$rc" >&2
   return $rc
 }
 for step in "$@"; do

@@ -18,7 +18,8 @@ for k, p in sorted(b.get("proxy_8gpu", {}).items()):
     if not isinstance(p, dict):
         continue
     sh = " | ".join(f"r{s['rank']}: V={s['local_nodes']} vb={s['vb']} H={s['halo_rows']} E={s['stored_edges']} "
-                    f"{s['ms_per_step']:.2f} ms + ex {s['exchange']['ms_direct']:.2f} ({s['exchange']['mode']})"
+                    f"{s['ms_per_step']:.2f} ms (cons {s.get('consensus_ms', float('nan')):.2f}) + ex "
+                    f"{s['exchange']['ms_direct']:.2f} ({s['exchange']['mode']})"
                     for s in p["shares"])
     print(f"proxy {k}: T1 {p['T1_ms_per_step']:.2f} ms, per-node ratio {p['per_node_cost_ratio']:.3f}, "
           f"speedup {p['predicted_speedup']:.2f}x (one link {p['predicted_speedup_one_link']:.2f}x)  [{sh}]")
