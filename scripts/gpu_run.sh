@@ -3,7 +3,7 @@
 # usage: bash scripts/gpu_run.sh TAG STEP [STEP ...]
 #   pmc        PMC HBM passes of the C3 headline and the weak8 share -> profiles/TAG_traffic*.json
 #   tests=EXPR pytest -m gpu -k EXPR (EXPR "all": every gpu test)
-#   prof       rocprofv3 --kernel-trace --stats of the headline -> gpurun_out/prof_TAG
+#   prof[m]    rocprofv3 --kernel-trace --stats of the headline -> gpurun_out/prof[m]_TAG (m: mirror)
 #   bench      the default bench line (CPU baseline, weak8, strong C4, proxies fast)
 #   benchall   the default bench line with --proxy all (adds C5 on 8 ranks and C5 on one GPU)
 #   hl, hl2    headline only, no CPU baseline (--streams 1 / 2): quick A/B lines
@@ -35,9 +35,10 @@ for step in "$@"; do
       if [ "$expr" = all ]; then k=(); else k=(-k "$expr"); fi
       run pytest 1100 python -u -m pytest tests -m gpu "${k[@]}" -q -rf --timeout 600 --timeout-method thread --durations=15 > gpurun_out/pytest_${TAG}.log 2>&1
       rc=$?; tail -25 gpurun_out/pytest_${TAG}.log; [ $rc -ne 0 ] && exit $rc ;;
-    prof)
-      run prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --headline-only > gpurun_out/prof_${TAG}.log 2>&1 || exit 1
-      python scripts/top_kernels.py gpurun_out/prof_${TAG} ;;
+    prof|profm)  # profm: with the mirror-mode forward
+      mm=0; [ $step = profm ] && mm=1
+      ADMM_FWD_MIRROR=$mm run $step 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${step}_${TAG} -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --headline-only > gpurun_out/${step}_${TAG}.log 2>&1 || exit 1
+      python scripts/top_kernels.py gpurun_out/${step}_${TAG} ;;
     bench)
       run bench 600 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || { tail -5 gpurun_out/bench_${TAG}.err; exit 1; }
       python scripts/summarize_bench.py gpurun_out/bench_${TAG}.json ;;

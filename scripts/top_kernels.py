@@ -8,6 +8,6 @@ if not paths:
     sys.exit(f"no kernel_stats.csv under {sys.argv[1]}")
 with open(paths[0]) as f:
     rows = list(csv.DictReader(f))
-for r in rows[:12]:
+for r in rows[:16]:
     name = r["Name"].split("(")[0].replace("void admm::", "")
     print(f"{float(r['AverageNs']) / 1e3:8.2f} us x{int(r['Calls']):5d} {float(r['Percentage']):6.2f}%  {name}")
