@@ -238,7 +238,16 @@ def cpu_baseline(N, a, b, q, x_gpu, procs=None, budget=CPU_BASELINE_SECONDS):
 # figure depends on the node chunks one launch projects.  PMC counters cannot be read
 # inside this run.
 TRAFFIC_FILES = {"C3": "profiles/r4_traffic.json", "weak8": "profiles/r4_traffic_weak8.json"}
-FWD_KERNEL = "admm::k_fwdg<float, 8>"
+
+
+def fwd_kernel_traffic(tr, tname, vb, mirror):
+    """PMC bytes per launch of the batch's forward projector instantiation
+    (k_fwdg<T, VB, MIRROR, VBR>; mirror mode projects virtual width 2 x VBR)."""
+    if not tr:
+        return None
+    want = f"admm::k_fwdg<{tname}, {min(2 * vb, 32 // (8 if tname == 'double' else 4)) if mirror else vb}, " \
+           f"{'true' if mirror else 'false'}, {vb}>"
+    return tr["kernels"].get(want, {}).get("hbm_bytes_per_launch")
 
 
 def pmc_traffic(workload):
@@ -476,7 +485,7 @@ def forward_roofline(r, workload, fwd_reps):
     as_designed = 2 * V * n * sbytes + 8 * V * m * sbytes  # image + transposed copy, 8 segment partials
     lds_bytes = sbytes * a_node * n_img * 2 * n_img * V  # m rays x N rows x 2 taps x V samples
     tr, tr_file = pmc_traffic(workload)
-    fwd_traffic = tr["kernels"].get(FWD_KERNEL, {}).get("hbm_bytes_per_launch") if tr else None
+    fwd_traffic = fwd_kernel_traffic(tr, "double" if dtype == "float64" else "float", nb.ctx_vb, nb.mirror)
     fwd_s = fwd_ms * 1e-3
     roof = {
         "kernel": f"k_fwdg<{'double' if dtype == 'float64' else 'float'},{nb.ctx_vb}> (Joseph forward "

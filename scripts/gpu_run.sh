@@ -50,6 +50,10 @@ for step in "$@"; do
       mm=0; case $step in hlm*) mm=1 ;; esac
       ADMM_FWD_MIRROR=$mm run $step 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --headline-only --streams $st > gpurun_out/${step}_${TAG}.json 2> gpurun_out/${step}_${TAG}.err || { tail -5 gpurun_out/${step}_${TAG}.err; exit 1; }
       python scripts/summarize_bench.py gpurun_out/${step}_${TAG}.json ;;
+    var=*)  # var=NAME[:m]: headline with the tuning build variants/libadmm_NAME.so (m: mirror mode)
+      v=${step#var=}; mm=0; case $v in *:m) mm=1; v=${v%:m} ;; esac
+      ADMM_TOMO_LIB=variants/libadmm_$v.so ADMM_FWD_MIRROR=$mm run $step 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --headline-only > gpurun_out/var_${v}_${mm}_${TAG}.json 2> gpurun_out/var_${v}_${mm}_${TAG}.err || { tail -5 gpurun_out/var_${v}_${mm}_${TAG}.err; exit 1; }
+      python scripts/summarize_bench.py gpurun_out/var_${v}_${mm}_${TAG}.json ;;
     benchallm)  # benchall with the mirror-mode forward
       ADMM_FWD_MIRROR=1 run benchallm 900 python bench.py --steps 20 --warmup 5 --proxy all --no-cpu-baseline > gpurun_out/benchallm_${TAG}.json 2> gpurun_out/benchallm_${TAG}.err || { tail -5 gpurun_out/benchallm_${TAG}.err; exit 1; }
       python scripts/summarize_bench.py gpurun_out/benchallm_${TAG}.json ;;
