@@ -117,6 +117,8 @@ struct admm_ctx {
   int plan_n[kPlans] = {}, plan_blocks[kPlans] = {};
   double plan_staged[kPlans] = {};      // touched row pixels staged per node chunk (host model)
   std::vector<int4> plan_blk[kPlans];  // per block: {ray-range index, group, segment, G}
+  std::vector<char> plan_caseA[kPlans];  // per group: its angles read the transposed image
+  bool mirror_half = false;  // the half geometry of a mirror-mode context (XCD mapping below)
   Buf fg_order;                       // int4 block table of the grouped forward projector
   int fg_nblk = 0, fg_order_nch = 0;
   hipStream_t cap = nullptr;  // private capture stream
@@ -210,8 +212,22 @@ int build_fwd_order_into(admm_ctx* C, int pl, int nch, int cus, Buf& buf, int* n
     // holds one band of image rows (and of the transposed copy) instead of re-fetching the
     // whole image from the Infinity Cache (LDS-DMA staging reads ~10x the image per launch).
     // Per XCD: heaviest first, the second round reversed (heavy + light per CU pair).
+    // Mirror mode (the half geometry): a case-B block of segment s stages rows of band s
+    // (virtual plane 0) and of band kFgSeg-1-s (plane 1, row N-1-m), a case-A block only
+    // band s of the transposed image (plane 1 mirrors the column).  Segments s and
+    // kFgSeg-1-s therefore share an XCD pair: one XCD takes their case-B blocks, the other
+    // their case-A blocks, so each band of either image lives in one L2 (segment-per-XCD put
+    // every img band in two L2s: FETCH_SIZE 2x, profiles/r4_mirror_xcd.txt).
+    const char* mx = getenv("ADMM_FWD_MIRROR_XCD");  // "0": segment-per-XCD (A/B)
+    const bool paired = C->mirror_half && !(mx && mx[0] == '0');
+    auto xcd_of = [&](const int4& b) {
+      const int sg = b.z % kFgSeg;
+      if (!paired) return sg % kXcds;
+      const int pair = std::min(sg, kFgSeg - 1 - sg);
+      return (2 * pair + (C->plan_caseA[pl][b.y] ? 1 : 0)) % kXcds;
+    };
     std::vector<std::vector<Blk>> L(kXcds);
-    for (const Blk& b : v) L[(b.b.z % kFgSeg) % kXcds].push_back(b);
+    for (const Blk& b : v) L[xcd_of(b.b)].push_back(b);
     for (auto& l : L) by_weight(l, cus / kXcds);
     std::vector<size_t> pos(kXcds, 0);
     v.clear();
@@ -242,30 +258,29 @@ int build_fwd_order(admm_ctx* C, int pl, int nch, int cus) {
   return ADMM_OK;
 }
 
-// Forward plan for the bound batch: the ray-aligned plan stages less per tap but has one
-// more chunk per (group, segment); take it unless the busiest CU would host more of its
-// blocks (e.g. 512^2: 512 unaligned blocks put 2 on every one of 256 CUs, the aligned 528
-// put 3 on some; co-resident blocks share the CU).  When that plan needs more than one round
-// of blocks, the plan staging the fewest pixels replaces it (1024^2, 2048^2: the chunk-
-// aligned plan with clipped rays, 107 / 870 us against 130 / 1020 for the best unclipped
-// one); in one round the 64-ray plan's equal segment shares keep every XCD on its own
-// row band (512^2: 31.2 us; the clipped plans' 440-492 blocks run 35.5-37).
+// Forward plan for the bound batch, by rounds of resident blocks: a launch of B blocks on
+// S = (blocks per CU) x CUs slots runs ceil(B / S) rounds, and a partial last round costs
+// nearly a full one (C3 mirror mode: 1024 / 992 blocks = 2 rounds, 65 us; 1056-1296 = 3
+// rounds, 74-84 us; profiles/r4_fwd_plan_rounds.txt).  Among the plans with the fewest
+// rounds, the one staging the fewest row pixels (1024^2, 2048^2: the chunk-aligned plan with
+// clipped rays, 107 / 870 us against 130 / 1020 for the best unclipped one) -- except in a
+// single round, where the 64-ray plan's equal segment shares keep every XCD on its own row
+// band (512^2, one chunk: 33 us against 35-37 for the clipped plans).
 // ADMM_FWD_PLAN=0..5 forces a plan.
-// (The occupancy query only guards against a plan that cannot be resident at all.)
 template <typename T, int VB>
 int pick_fwd_plan(admm_ctx* C, int nch, int* pl_out, int* cus_out) {
   int per_cu = 0, cus = 0;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fwdg<T, VB>, kFgThreads, 0));
   HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, C->device));
   if (per_cu < 1) return fail(ADMM_E_HIP, "grouped forward projector cannot be resident");
-  auto per_cu_max = [&](int pl) { return ((long)C->plan_blocks[pl] * nch + cus - 1) / std::max(1, cus); };
-  int pl = per_cu_max(1) <= per_cu_max(0) ? 1 : 0;
-  if (per_cu_max(pl) > per_cu) {
-    // more than one round of blocks: the plan staging the fewest row pixels (large images,
-    // where staging from beyond L2 and the rays missing a segment dominate)
-    for (int q = 0; q < admm_ctx::kPlans; ++q)
-      if (C->plan_n[q] > 0 && C->plan_staged[q] < C->plan_staged[pl]) pl = q;
+  const long slots = (long)per_cu * std::max(1, cus);
+  auto rounds = [&](int pl) { return ((long)C->plan_blocks[pl] * nch + slots - 1) / slots; };
+  int pl = 0;
+  for (int q = 1; q < admm_ctx::kPlans; ++q) {
+    if (C->plan_n[q] == 0) continue;
+    if (rounds(q) < rounds(pl) || (rounds(q) == rounds(pl) && C->plan_staged[q] < C->plan_staged[pl])) pl = q;
   }
+  if (rounds(pl) == 1 && rounds(0) == 1) pl = 0;
   const char* f = getenv("ADMM_FWD_PLAN");
   if (f && f[0] >= '0' && f[0] < '0' + admm_ctx::kPlans && C->plan_n[f[0] - '0'] > 0) pl = f[0] - '0';
   *pl_out = pl;
@@ -333,6 +348,7 @@ int bind_fwd_plan(admm_ctx* C, int V) {
     hg.n_angles = C->g.n_angles / 2;
     hg.angle_max = C->g.angle_min + 0.5 * (C->g.angle_max - C->g.angle_min);
     RET(admm_ctx_create(&C->half, &hg, C->dtype, 1, C->device));  // (tables and plans only)
+    C->half->mirror_half = true;
     if (C->half->n_groups == 0) C->mm = false;  // (cannot happen: half the angles fit as well)
   }
   if (C->mm) {
@@ -1103,6 +1119,8 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
       HIPCHK(hipMalloc(&C->plan_rng[pl], rv.size() * sizeof(FgRange)));
       HIPCHK(hipMemcpy(C->plan_rng[pl], rv.data(), rv.size() * sizeof(FgRange), hipMemcpyHostToDevice));
       C->plan_blk[pl] = blk_plan[pl];
+      C->plan_caseA[pl].clear();
+      for (const FgGroup& gr : gv) C->plan_caseA[pl].push_back(fa[gr.t0].caseA != 0);
       C->plan_n[pl] = (int)gv.size();
       C->plan_blocks[pl] = (int)blk_plan[pl].size();
       C->plan_staged[pl] = staged_plan[pl];

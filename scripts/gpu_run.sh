@@ -30,6 +30,10 @@ for step in "$@"; do
       WORKLOAD=weak8 run pmc_weak8 400 bash scripts/pmc.sh ${TAG}w8 > gpurun_out/pmc_${TAG}w8.log 2>&1 || { tail -5 gpurun_out/pmc_${TAG}w8.log; exit 1; }
       cp gpurun_out/${TAG}w8_traffic.json profiles/${TAG}_traffic_weak8.json
       tail -12 gpurun_out/pmc_${TAG}.log ;;
+    sq|sqm)  # FETCH_SIZE + SQ counters of the headline (scripts/passes_fwd_sq.txt); m: mirror mode
+      mm=0; [ $step = sqm ] && mm=1
+      ADMM_FWD_MIRROR=$mm PASSFILE=scripts/passes_fwd_sq.txt run $step 600 bash scripts/pmc.sh ${step}_${TAG} > gpurun_out/${step}_${TAG}.log 2>&1 || { tail -5 gpurun_out/${step}_${TAG}.log; exit 1; }
+      python scripts/pmc_summary.py ${step}_${TAG} "k_fwdg<" "k_back" ;;
     tests=*)
       expr=${step#tests=}
       if [ "$expr" = all ]; then k=(); else k=(-k "$expr"); fi
@@ -54,6 +58,10 @@ for step in "$@"; do
       v=${step#var=}; mm=0; case $v in *:m) mm=1; v=${v%:m} ;; esac
       ADMM_TOMO_LIB=variants/libadmm_$v.so ADMM_FWD_MIRROR=$mm run $step 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --headline-only > gpurun_out/var_${v}_${mm}_${TAG}.json 2> gpurun_out/var_${v}_${mm}_${TAG}.err || { tail -5 gpurun_out/var_${v}_${mm}_${TAG}.err; exit 1; }
       python scripts/summarize_bench.py gpurun_out/var_${v}_${mm}_${TAG}.json ;;
+    plan=*)  # plan=K[:m]: headline with the forward plan forced to K (ADMM_FWD_PLAN; m: mirror mode)
+      v=${step#plan=}; mm=0; case $v in *:m) mm=1; v=${v%:m} ;; esac
+      ADMM_FWD_PLAN=$v ADMM_FWD_MIRROR=$mm run $step 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --headline-only > gpurun_out/plan_${v}_${mm}_${TAG}.json 2> gpurun_out/plan_${v}_${mm}_${TAG}.err || { tail -5 gpurun_out/plan_${v}_${mm}_${TAG}.err; exit 1; }
+      python scripts/summarize_bench.py gpurun_out/plan_${v}_${mm}_${TAG}.json ;;
     benchallm)  # benchall with the mirror-mode forward
       ADMM_FWD_MIRROR=1 run benchallm 900 python bench.py --steps 20 --warmup 5 --proxy all --no-cpu-baseline > gpurun_out/benchallm_${TAG}.json 2> gpurun_out/benchallm_${TAG}.err || { tail -5 gpurun_out/benchallm_${TAG}.err; exit 1; }
       python scripts/summarize_bench.py gpurun_out/benchallm_${TAG}.json ;;
