@@ -316,14 +316,19 @@ template <typename T, int VBR>
 constexpr int mirror_vb() {
   return 2 * VBR < 32 / (int)sizeof(T) ? 2 * VBR : 32 / (int)sizeof(T);
 }
-// Mirror mode applies to the geometry, not the batch (so every node runs the same arithmetic
-// whatever its batch's size: rank- and batch-invariant results): an even number of angles
-// spanning [0, pi) (block_2_load_odl_data.py:51) and a detector symmetric about 0
-// (block_2:52, uniform_partition(-1, 1, N)).  ADMM_FWD_MIRROR=1 switches it on (A/B).
+// Mirror mode applies to the geometry and sample type, never to the batch (so every node runs
+// the same arithmetic whatever its batch's size: rank- and batch-invariant results): an even
+// number of angles spanning [0, pi) (block_2_load_odl_data.py:51) and a detector symmetric
+// about 0 (block_2:52, uniform_partition(-1, 1, N)).  On by default for float32 samples
+// (C3: 62 vs 57 us per forward launch at 16 nodes, but a 4-node rank of C4 on 8 GPUs runs
+// 9.4 instead of 11.5 ms per iteration: profiles/r4_mirror_ab.txt); float64 (C5: 2 real
+// nodes per 16-byte vector) measured slower in both widths, so opt-in there.
+// ADMM_FWD_MIRROR=0 / 1 forces it off / on.
 bool mirror_eligible(const admm_ctx* C) {
   if (C->csr || C->g.n_angles < 2 || C->g.n_angles % 2 != 0) return false;
   const char* e = getenv("ADMM_FWD_MIRROR");
-  if (!(e && e[0] == '1')) return false;  // (opt-in until measured)
+  const bool want = (e && e[0]) ? e[0] == '1' : C->dtype == ADMM_DTYPE_F32;
+  if (!want) return false;
   const double pi = 3.14159265358979323846;
   return std::fabs(C->g.angle_min) <= 1e-15 && std::fabs(C->g.angle_max - pi) <= 1e-12 &&
          std::fabs(C->g.det_min + C->g.det_max) <= 1e-12 * std::fabs(C->g.det_max);

@@ -6,7 +6,8 @@
 #   prof[m]    rocprofv3 --kernel-trace --stats of the headline -> gpurun_out/prof[m]_TAG (m: mirror)
 #   bench      the default bench line (CPU baseline, weak8, strong C4, proxies fast)
 #   benchall   the default bench line with --proxy all (adds C5 on 8 ranks and C5 on one GPU)
-#   hl, hl2    headline only, no CPU baseline (--streams 1 / 2): quick A/B lines
+#   hl, hl2    headline only, no CPU baseline (--streams 1 / 2), mirror mode forced off: quick A/B lines
+#   hlm        the same with the mirror mode forced on (the float32 default)
 #   configs    bench.py --config C2 C3 C4 C5s
 #   smoke      __graft_entry__.smoke()
 # Every step has its own time limit; the first failing step ends the session.
@@ -39,8 +40,8 @@ for step in "$@"; do
       if [ "$expr" = all ]; then k=(); else k=(-k "$expr"); fi
       run pytest 1100 python -u -m pytest tests -m gpu "${k[@]}" -q -rf --timeout 600 --timeout-method thread --durations=15 > gpurun_out/pytest_${TAG}.log 2>&1
       rc=$?; tail -25 gpurun_out/pytest_${TAG}.log; [ $rc -ne 0 ] && exit $rc ;;
-    prof|profm)  # profm: with the mirror-mode forward
-      mm=0; [ $step = profm ] && mm=1
+    prof|profm|profd)  # prof: default modes; profm / profd: mirror-mode forward forced on / off
+      mm=; [ $step = profm ] && mm=1; [ $step = profd ] && mm=0
       ADMM_FWD_MIRROR=$mm run $step 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${step}_${TAG} -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --headline-only > gpurun_out/${step}_${TAG}.log 2>&1 || exit 1
       python scripts/top_kernels.py gpurun_out/${step}_${TAG} ;;
     bench)

@@ -1,4 +1,5 @@
-"""GPU: mirror mode of the forward projector (ADMM_FWD_MIRROR=1; kernels.hpp k_fwdg MIRROR).
+"""GPU: mirror mode of the forward projector (kernels.hpp k_fwdg MIRROR; the float32 default,
+ADMM_FWD_MIRROR=0 / 1 forces it off / on).
 
 Angle a-1-t projects I as angle t projects flipud(I) (tests/test_oracle.py::
 test_mirror_symmetry_of_the_joseph_operator), so a batch projects virtual images -- its real
@@ -40,10 +41,13 @@ def _run(N, V, a_per, dtype, iters=3, graph="ring"):
     return ops, ph, sinos, Q, G, np.stack(x), h
 
 
-@pytest.mark.parametrize("dtype,V", [("float32", 1), ("float32", 2), ("float32", 4), ("float32", 8),
-                                     ("float32", 12), ("float64", 1), ("float64", 2), ("float64", 4)])
-def test_mirror_trajectory_matches_oracle(cuda, monkeypatch, dtype, V):
-    monkeypatch.setenv("ADMM_FWD_MIRROR", "1")
+@pytest.mark.parametrize("dtype,V,mode", [("float32", 1, "1"), ("float32", 2, "1"), ("float32", 4, "1"),
+                                          ("float32", 8, "1"), ("float32", 12, "1"), ("float64", 1, "1"),
+                                          ("float64", 2, "1"), ("float64", 4, "1"),
+                                          ("float32", 4, "0"), ("float32", 12, "0")])
+def test_mirror_trajectory_matches_oracle(cuda, monkeypatch, dtype, V, mode):
+    """mode "1": mirror mode at every node-interleave width; "0": the direct projection."""
+    monkeypatch.setenv("ADMM_FWD_MIRROR", mode)
     N, a = 48, 24
     ops, ph, sinos, Q, G, x, h = _run(N, V, a, dtype)
     A = joseph_matrix(Geometry(N, a))
@@ -59,12 +63,13 @@ def test_mirror_trajectory_matches_oracle(cuda, monkeypatch, dtype, V):
     assert all(v < tol for v in errs.values()), errs
 
 
-@pytest.mark.parametrize("dtype", ["float32", "float64"])
-def test_mirror_result_independent_of_batch_size(cuda, monkeypatch, dtype):
+@pytest.mark.parametrize("dtype,mode", [("float32", "1"), ("float64", "1"), ("float32", "0")])
+def test_mirror_result_independent_of_batch_size(cuda, monkeypatch, dtype, mode):
     """Node 0 of an edgeless graph (its x-update sees only its own data) in batches of 1, 2,
     3, 4, 8 nodes -- every node-interleave width and both staging paths (LDS-DMA and the
-    register path of the narrow widths) -- bitwise the same image and statistics."""
-    monkeypatch.setenv("ADMM_FWD_MIRROR", "1")
+    register path of the narrow widths) -- bitwise the same image and statistics (mirror
+    mode, and the direct projection)."""
+    monkeypatch.setenv("ADMM_FWD_MIRROR", mode)
     res = {}
     for V in (1, 2, 3, 4, 8):
         _, _, _, _, _, x, h = _run(40, V, 16, dtype, iters=2, graph="empty")
@@ -87,3 +92,20 @@ def test_mirror_is_the_direct_projection_to_rounding(cuda, monkeypatch):
         monkeypatch.setenv("ADMM_FWD_MIRROR", mode)
         out["odd" + mode] = _run(48, 4, 23, "float32")[5]
     assert np.array_equal(out["odd0"], out["odd1"])
+
+
+def test_default_mode_by_sample_type(cuda, monkeypatch):
+    """Unset ADMM_FWD_MIRROR: mirror mode for float32 samples (every batch width, 16-byte real
+    vectors), the direct projection for float64; odd angle counts never mirror."""
+    from admm_hip.plan import make_plan
+    from admm_hip.solver import NodeBatch
+    monkeypatch.delenv("ADMM_FWD_MIRROR", raising=False)
+    for dtype, V, a, want, vb in [("float32", 8, 24, True, 4), ("float32", 3, 24, True, 4),
+                                  ("float32", 8, 23, False, 8), ("float64", 4, 24, False, 4)]:
+        ops = make_operators(40, V, a * V, dtype=dtype, device=0)
+        ph = shepp_logan(40)
+        plan = make_plan(nx.cycle_graph(V), V)
+        sinos = dict(zip(plan.local_nodes, make_sinograms(ops, ph, 0.005, seed=3)))
+        _, Q = make_precisions(ops)
+        nb = NodeBatch(ops[0].geom, dtype, plan, sinos, Q, 2.0, 0.02, 0.2, 3, 3, "iso", ph, 0)
+        assert nb.mirror == want and nb.ctx_vb == vb, (dtype, V, a, nb.mirror, nb.ctx_vb)
