@@ -485,12 +485,15 @@ def forward_roofline(r, workload, fwd_reps):
     as_designed = 2 * V * n * sbytes + 8 * V * m * sbytes  # image + transposed copy, 8 segment partials
     lds_bytes = sbytes * a_node * n_img * 2 * n_img * V  # m rays x N rows x 2 taps x V samples
     tr, tr_file = pmc_traffic(workload)
-    fwd_traffic = fwd_kernel_traffic(tr, "double" if dtype == "float64" else "float", nb.ctx_vb, nb.mirror)
+    tname = "double" if dtype == "float64" else "float"
+    vbv = min(2 * nb.ctx_vb, 32 // sbytes)  # mirror mode's virtual width
+    fwd_traffic = fwd_kernel_traffic(tr, tname, nb.ctx_vb, nb.mirror)
     fwd_s = fwd_ms * 1e-3
     roof = {
-        "kernel": f"k_fwdg<{'double' if dtype == 'float64' else 'float'},{nb.ctx_vb}> (Joseph forward "
-                  f"projector taps, angle-grouped, 8 row-segment partial sums per ray; {V} nodes = "
-                  f"{-(-V // nb.ctx_vb)} node chunk(s) per launch)",
+        "kernel": (f"k_fwdg<{tname},{vbv},true,{nb.ctx_vb}> (mirror mode: virtual {vbv}-lane images over half "
+                   f"the angles; " if nb.mirror else f"k_fwdg<{tname},{nb.ctx_vb}> (")
+                  + f"Joseph forward projector taps, angle-grouped, 8 row-segment partial sums per ray; {V} nodes "
+                  f"= {-(-V // nb.ctx_vb)} node chunk(s) per launch)",
         # the angle-group plan the batch bound (admm_fwd_plan_info): 0 = 64-ray chunks,
         # 1 = aligned per (segment, angle), 2 = aligned per (segment, chunk); 3-5 = clipped
         "fwd_plan": next((dict(p) for p in nb.fwd_plans() if p["active"]), None),
