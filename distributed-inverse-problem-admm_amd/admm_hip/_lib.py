@@ -127,7 +127,7 @@ def load(path: str | None = None):
     with _lock:
         if _lib is not None and path is None:
             return _lib
-        p = path or os.environ.get("ADMM_TOMO_LIB", LIB_PATH)
+        p = path or os.environ.get("ADMM_TOMO_LIB") or LIB_PATH
         if not os.path.exists(p):
             raise AdmmLibraryError(
                 f"{p} not found: build the HIP extension first "

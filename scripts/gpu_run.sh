@@ -55,10 +55,12 @@ for step in "$@"; do
       mm=0; case $step in hlm*) mm=1 ;; esac
       ADMM_FWD_MIRROR=$mm run $step 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --headline-only --streams $st > gpurun_out/${step}_${TAG}.json 2> gpurun_out/${step}_${TAG}.err || { tail -5 gpurun_out/${step}_${TAG}.err; exit 1; }
       python scripts/summarize_bench.py gpurun_out/${step}_${TAG}.json ;;
-    var=*)  # var=NAME[:m]: headline with the tuning build variants/libadmm_NAME.so (m: mirror mode)
-      v=${step#var=}; mm=0; case $v in *:m) mm=1; v=${v%:m} ;; esac
-      ADMM_TOMO_LIB=variants/libadmm_$v.so ADMM_FWD_MIRROR=$mm run $step 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --headline-only > gpurun_out/var_${v}_${mm}_${TAG}.json 2> gpurun_out/var_${v}_${mm}_${TAG}.err || { tail -5 gpurun_out/var_${v}_${mm}_${TAG}.err; exit 1; }
-      python scripts/summarize_bench.py gpurun_out/var_${v}_${mm}_${TAG}.json ;;
+    var=*)  # var=NAME[@WORKLOAD]: headline (C3 or weak8) with the tuning build variants/lib_NAME.so
+            # (scripts/sweep_build.py; NAME "base": the in-tree library), default modes
+      v=${step#var=}; wl=C3; case $v in *@*) wl=${v#*@}; v=${v%@*} ;; esac
+      lib=variants/lib_$v.so; [ $v = base ] && lib=
+      ADMM_TOMO_LIB=$lib run $step 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --headline-only --workload $wl > gpurun_out/var_${v}_${wl}_${TAG}.json 2> gpurun_out/var_${v}_${wl}_${TAG}.err || { tail -5 gpurun_out/var_${v}_${wl}_${TAG}.err; exit 1; }
+      python scripts/summarize_bench.py gpurun_out/var_${v}_${wl}_${TAG}.json ;;
     plan=*)  # plan=K[:m]: headline with the forward plan forced to K (ADMM_FWD_PLAN; m: mirror mode)
       v=${step#plan=}; mm=0; case $v in *:m) mm=1; v=${v%:m} ;; esac
       ADMM_FWD_PLAN=$v ADMM_FWD_MIRROR=$mm run $step 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --headline-only > gpurun_out/plan_${v}_${mm}_${TAG}.json 2> gpurun_out/plan_${v}_${mm}_${TAG}.err || { tail -5 gpurun_out/plan_${v}_${mm}_${TAG}.err; exit 1; }
@@ -66,6 +68,12 @@ for step in "$@"; do
     benchallm)  # benchall with the mirror-mode forward
       ADMM_FWD_MIRROR=1 run benchallm 900 python bench.py --steps 20 --warmup 5 --proxy all --no-cpu-baseline > gpurun_out/benchallm_${TAG}.json 2> gpurun_out/benchallm_${TAG}.err || { tail -5 gpurun_out/benchallm_${TAG}.err; exit 1; }
       python scripts/summarize_bench.py gpurun_out/benchallm_${TAG}.json ;;
+    share=*)  # share=CONFIG:R/W[:z]: one rank's share on this GPU (bench --as-rank; z: --stored-z A/B)
+      v=${step#share=}; cfg=${v%%:*}; rest=${v#*:}; rw=${rest%%:*}; sz=()
+      case $rest in *:z) sz=(--stored-z) ;; esac
+      out=gpurun_out/share_${cfg}_${rw/\//of}${sz:+_z}_${TAG}.json
+      run $step 600 python bench.py --config $cfg --as-rank $rw --steps 4 --warmup 2 "${sz[@]}" > $out 2> ${out%.json}.err || { tail -5 ${out%.json}.err; exit 1; }
+      tail -c 600 $out ;;
     configs)
       run configs 1000 bash scripts/run_configs.sh C2 C3 C4 C5s || exit 1 ;;
     smoke)

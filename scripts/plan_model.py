@@ -1,6 +1,6 @@
 """Host-side model of the grouped forward projector's angle-group planner (admm_tomo.hip,
 admm_ctx_create: plan_group / the greedy loop) for sweeping its parameters without a GPU.
-usage: python scripts/plan_model.py N ANGLES SEGMENTS GMAX WIN RAYS
+usage: python scripts/plan_model.py N ANGLES SEGMENTS GMAX WIN RAYS [FULL_ANGLES]
 Prints, for the unaligned and the ray-aligned plan: group sizes, blocks, touched row pixels
 per launch (staged_px) and pixels fetched by the 64-slot LDS-DMA pieces (fetched_px; MB at
 32 B per pixel = 8 float32 nodes)."""
@@ -11,11 +11,12 @@ SEG = int(sys.argv[3]) if len(sys.argv) > 3 else 8
 GMAX = int(sys.argv[4]) if len(sys.argv) > 4 else 16
 WIN = int(sys.argv[5]) if len(sys.argv) > 5 else 256
 RAYS = int(sys.argv[6]) if len(sys.argv) > 6 else 64
+NFULL = int(sys.argv[7]) if len(sys.argv) > 7 else NA  # angle step pi/NFULL (mirror half: NA = NFULL/2)
 ndet = N
 h = 2.0 / N; hd = 2.0 / ndet; c0 = 0.5 * (N - 1); det_min = -1.0
 fa = []
 for t in range(NA):
-    th = (t + 0.5) * math.pi / NA
+    th = (t + 0.5) * math.pi / NFULL
     cs, sn = math.cos(th), math.sin(th)
     caseA = abs(cs) >= abs(sn)
     al, be = (cs, sn) if caseA else (sn, cs)
