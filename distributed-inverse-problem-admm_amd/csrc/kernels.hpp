@@ -767,7 +767,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
     // unit serves all 32 waves, and the mirror kernel's DMA block spent 30 scalar instructions
     // per chunk (the direct kernel's 18).  Same rows, columns and slots: bitwise the same staging.
     static_assert(PIECES <= kFgG, "one LDS-DMA piece per wave and chunk");
-    const bool has_piece = g < PIECES;
+    const bool has_piece = PIECES == kFgG || g < PIECES;  // (every wave has one at 16 pieces)
     const int ph = g % kFgPieces, ppar = (g / kFgPieces) & 1, prp = g / (2 * kFgPieces);
     const int pr = prp % R, ppl = prp / R;
     const bool prow_rev = MIRROR && ppl == 1 && !caseA;  // case B from row N-1-m
@@ -780,12 +780,15 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
     // lane part of the staged column (the row's window origin is added per chunk); a mirrored
     // column N-1-(wo+c) is (N-1-c) - wo
     const int pcol = pcol_rev ? N - 1 - (128 * ph + ppar + 2 * lane) : 128 * ph + ppar + 2 * lane;
-    // dma(m0, b): chunk m0's piece into buffer b.  Called once per chunk with m0 ascending by R
-    // from m_lo (the running row address relies on it).
-    auto dma = [&](int m0, int b) {
+    const int psgn = pcol_rev ? -1 : 1;  // (one scalar multiply per chunk instead of a select)
+    // dma(m0, b[, full]): chunk m0's piece into buffer b; full (compile time): the chunk is
+    // known to have all R rows.  Called once per chunk with m0 ascending by R from m_lo (the
+    // running row address relies on it).
+    auto dma = [&](int m0, int b, auto fullc) {
       const char* rowp = prow;
       prow += rstep;
-      if (!has_piece || pr >= m_hi - m0) return;  // no piece / row past the segment
+      if (!has_piece) return;
+      if (!decltype(fullc)::value && pr >= m_hi - m0) return;  // row past the segment
       const int wo = __builtin_amdgcn_readfirstlane(wlo_s[m0 - m_lo + pr]);
       const int wn = __builtin_amdgcn_readfirstlane(wnum_s[m0 - m_lo + pr]);
       if (128 * ph + ppar >= wn) return;  // piece wholly past the touched width
@@ -795,7 +798,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)rb);
       const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(rb >> 32));
       const __amdgpu_buffer_rsrc_t rs = make_rsrc((const void*)(uintptr_t)(((uint64_t)hi << 32) | lo), rowbytes);
-      const int col = pcol_rev ? pcol - wo : pcol + wo;
+      const int col = pcol + psgn * wo;
       // negative columns wrap to huge unsigned offsets: out of range, zero-filled (slots past
       // the row's touched width are fetched but never read by a tap: masking them cost more
       // VALU than the L2 fetch it saved)
@@ -808,34 +811,58 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)&win1[ppl][pr][pslot],
                                                  16, voff, 0, 0, 0);
     };
-    dma(m_lo, 0);
+    dma(m_lo, 0, std::false_type{});
     __syncthreads();  // (its fence waits for this wave's LDS-DMA: vmcnt(0)) chunk 0 staged
     // one chunk: DMA of the next one into the other buffer, then this one's taps.  The
     // buffer index is a compile-time constant (the loop is unrolled by the two buffers), so
     // the LDS base of every tap read folds into the ds_read offset field instead of costing
     // two VALU adds per row (the kernel is VALU-issue bound)
-    auto step = [&](auto cbc, int m0) __attribute__((always_inline)) {
+    // FULL (compile time): the chunk has all R rows -- every chunk of the loop over chunk pairs;
+    // only a segment's last chunk can be short.  Idle waves skip the origins and the taps
+    // (wave-uniform branches; the row checks and selects they replace were scalar instructions
+    // on every chunk of every wave)
+    auto step = [&](auto cbc, auto fullc, int m0) __attribute__((always_inline)) {
       constexpr int cb = decltype(cbc)::value;
+      constexpr bool full = decltype(fullc)::value;
       // the other buffer was last read by the previous chunk's taps (done: barrier below)
-      if (m0 + R < m_hi) dma(m0 + R, cb ^ 1);
-      origins(m0, wl_cur);
-      const int rows = idle ? 0 : min(R, m_hi - m0);
-      if constexpr (cb == 0) {
-        if (rows == R)
-          taps4(win, m0);
-        else
-          taps(win, m0, rows, wl_cur);
-      } else {
-        if (rows == R)
-          taps4(win1, m0);
-        else
-          taps(win1, m0, rows, wl_cur);
+      // (in a full pair, chunk m0 + R of the first step is full too)
+      if (m0 + R < m_hi) dma(m0 + R, cb ^ 1, std::integral_constant<bool, full && cb == 0>{});
+      if (!idle) {
+        origins(m0, wl_cur);
+        if constexpr (full) {
+          if constexpr (cb == 0)
+            taps4(win, m0);
+          else
+            taps4(win1, m0);
+        } else {
+          const int rows = min(R, m_hi - m0);
+          if constexpr (cb == 0) {
+            if (rows == R)
+              taps4(win, m0);
+            else
+              taps(win, m0, rows, wl_cur);
+          } else {
+            if (rows == R)
+              taps4(win1, m0);
+            else
+              taps(win1, m0, rows, wl_cur);
+          }
+        }
       }
       __syncthreads();  // this chunk's readers done; next chunk's DMA landed (vmcnt(0) + barrier)
     };
-    for (int m0 = m_lo; m0 < m_hi; m0 += 2 * R) {
-      step(std::integral_constant<int, 0>{}, m0);
-      if (m0 + R < m_hi) step(std::integral_constant<int, 1>{}, m0 + R);
+    using C0 = std::integral_constant<int, 0>;
+    using C1 = std::integral_constant<int, 1>;
+    using Full = std::true_type;
+    using Part = std::false_type;
+    int m0 = m_lo;
+    for (; m0 + 2 * R <= m_hi; m0 += 2 * R) {
+      step(C0{}, Full{}, m0);
+      step(C1{}, Full{}, m0 + R);
+    }
+    if (m0 < m_hi) {  // the segment's last one or two chunks (the last one may be short)
+      step(C0{}, Part{}, m0);
+      if (m0 + R < m_hi) step(C1{}, Part{}, m0 + R);
     }
   } else {
     // staging in two halves: issue global loads for chunk c+1 into registers

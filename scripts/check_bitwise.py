@@ -1,5 +1,5 @@
-"""Run one small ADMM solve (64^2, 5-node ring, 3 iterations, float32 samples) with the
-library ADMM_TOMO_LIB points to and save x / histories; with --compare A.npz B.npz report
+"""Run one small ADMM solve (64^2 or CHECK_N^2, 5-node ring, 3 iterations, float32 samples) with
+the library ADMM_TOMO_LIB points to and save x / histories; with --compare A.npz B.npz report
 whether two runs are bitwise equal (A/B of code paths that must not change results)."""
 import os
 import sys
@@ -22,7 +22,7 @@ from admm_hip.data import make_precisions, make_sinograms, shepp_logan  # noqa: 
 from admm_hip.solver import make_operators  # noqa: E402
 from block_6_admm_loop_ver2 import decentralized_admm  # noqa: E402
 
-N, V = 64, 5
+N, V = int(os.environ.get("CHECK_N", "64")), 5  # (N % 16 != 0: segments end in short chunks)
 ops = make_operators(N, V, angles_total=240, device=0)
 ph = shepp_logan(N)
 sinos = make_sinograms(ops, ph, 0.005)

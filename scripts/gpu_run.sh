@@ -74,6 +74,12 @@ for step in "$@"; do
       out=gpurun_out/share_${cfg}_${rw/\//of}${sz:+_z}_${TAG}.json
       run $step 600 python bench.py --config $cfg --as-rank $rw --steps 4 --warmup 2 "${sz[@]}" > $out 2> ${out%.json}.err || { tail -5 ${out%.json}.err; exit 1; }
       tail -c 600 $out ;;
+    bitwise=*)  # bitwise=NAME[:N]: scripts/check_bitwise.py with the in-tree library and variants/lib_NAME.so
+      v=${step#bitwise=}; n=64; case $v in *:*) n=${v#*:}; v=${v%%:*} ;; esac
+      CHECK_N=$n run bw_base 300 python scripts/check_bitwise.py gpurun_out/bw_base_${n}_${TAG}.npz > gpurun_out/bw_${v}_${n}_${TAG}.log 2>&1 &&
+      CHECK_N=$n ADMM_TOMO_LIB=variants/lib_$v.so run bw_$v 300 python scripts/check_bitwise.py gpurun_out/bw_${v}_${n}_${TAG}.npz >> gpurun_out/bw_${v}_${n}_${TAG}.log 2>&1 ||
+        { tail -5 gpurun_out/bw_${v}_${n}_${TAG}.log; exit 1; }
+      python scripts/check_bitwise.py --compare gpurun_out/bw_base_${n}_${TAG}.npz gpurun_out/bw_${v}_${n}_${TAG}.npz ;;
     configs)
       run configs 1000 bash scripts/run_configs.sh C2 C3 C4 C5s || exit 1 ;;
     smoke)
