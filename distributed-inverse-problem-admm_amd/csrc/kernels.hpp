@@ -759,57 +759,78 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
     // one 1-KiB piece per wave-instruction: 64 consecutive 16-B slots of one (plane, row,
     // parity half); a row's even half holds pixels wlo + 2s, its odd half wlo + 2s + 1
     const uint32_t rowbytes = (uint32_t)N * VBR * (uint32_t)sizeof(T);
-    // This wave's piece (PIECES <= kFgG: at most one per wave and chunk) is the same for every
-    // chunk of the segment -- its plane, row within the chunk, parity half, 64-slot piece and
-    // LDS slot are set once here -- and its staged row's address moves by a constant per chunk
-    // (mirror plane 1, case B: rows N-1-m, a negative step).  The address is kept as a running
-    // scalar base instead of a per-chunk 64-bit row multiply and row select: the CU's one scalar
-    // unit serves all 32 waves, and the mirror kernel's DMA block spent 30 scalar instructions
-    // per chunk (the direct kernel's 18).  Same rows, columns and slots: bitwise the same staging.
-    static_assert(PIECES <= kFgG, "one LDS-DMA piece per wave and chunk");
-    const bool has_piece = PIECES == kFgG || g < PIECES;  // (every wave has one at 16 pieces)
-    const int ph = g % kFgPieces, ppar = (g / kFgPieces) & 1, prp = g / (2 * kFgPieces);
-    const int pr = prp % R, ppl = prp / R;
-    const bool prow_rev = MIRROR && ppl == 1 && !caseA;  // case B from row N-1-m
-    const bool pcol_rev = MIRROR && ppl == 1 && caseA;   // case A: column N-1-w of the same row
-    const int pslot = (ppar ? kFgOdd : 0) + 64 * ph;
-    const long long rstride = (long long)rowbytes;
-    const char* prow = reinterpret_cast<const char*>(src) +
-                       (prow_rev ? (long long)(N - 1 - (m_lo + pr)) : (long long)(m_lo + pr)) * rstride;
-    const long long rstep = (prow_rev ? -rstride : rstride) * R;
-    // lane part of the staged column (the row's window origin is added per chunk); a mirrored
-    // column N-1-(wo+c) is (N-1-c) - wo
-    const int pcol = pcol_rev ? N - 1 - (128 * ph + ppar + 2 * lane) : 128 * ph + ppar + 2 * lane;
-    const int psgn = pcol_rev ? -1 : 1;  // (one scalar multiply per chunk instead of a select)
-    // dma(m0, b[, full]): chunk m0's piece into buffer b; full (compile time): the chunk is
-    // known to have all R rows.  Called once per chunk with m0 ascending by R from m_lo (the
-    // running row address relies on it).
+    // This wave's pieces (NPW = PIECES / kFgG per chunk: one for 2-row chunks) are the same for
+    // every chunk of the segment -- plane, row within the chunk, parity half, 64-slot piece and
+    // LDS slot are set once here -- and a piece's staged row moves by a constant per chunk
+    // (mirror plane 1, case B: rows N-1-m, a negative step).  The row address is kept as a
+    // running scalar base instead of a per-chunk 64-bit row multiply and row select: the CU's one
+    // scalar unit serves all 32 waves, and the mirror kernel's DMA block spent 30 scalar
+    // instructions per chunk (the direct kernel's 18).  Same rows, columns and slots: bitwise the
+    // same staging.
+    constexpr int NPW = (PIECES + kFgG - 1) / kFgG;
+    struct Piece {
+      bool has, rev_col;
+      int ph, ppar, pr, ppl, pslot, pcol, psgn;
+      const char* prow;
+      long long rstep;
+    };
+    Piece pc[NPW];
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) {
+      const int q = g + i * kFgG;
+      Piece& P = pc[i];
+      P.has = PIECES % kFgG == 0 || q < PIECES;  // (every wave has NPW at 16 / 32 pieces)
+      P.ph = q % kFgPieces;
+      P.ppar = (q / kFgPieces) & 1;
+      const int prp = q / (2 * kFgPieces);
+      P.pr = prp % R;
+      P.ppl = prp / R;
+      const bool prow_rev = MIRROR && P.ppl == 1 && !caseA;  // case B from row N-1-m
+      P.rev_col = MIRROR && P.ppl == 1 && caseA;             // case A: column N-1-w of the same row
+      P.pslot = (P.ppar ? kFgOdd : 0) + 64 * P.ph;
+      const long long rstride = (long long)rowbytes;
+      P.prow = reinterpret_cast<const char*>(src) +
+               (prow_rev ? (long long)(N - 1 - (m_lo + P.pr)) : (long long)(m_lo + P.pr)) * rstride;
+      P.rstep = (prow_rev ? -rstride : rstride) * R;
+      // lane part of the staged column (the row's window origin is added per chunk); a mirrored
+      // column N-1-(wo+c) is (N-1-c) - wo (a scalar multiply per chunk instead of a select)
+      const int c = 128 * P.ph + P.ppar + 2 * lane;
+      P.pcol = P.rev_col ? N - 1 - c : c;
+      P.psgn = P.rev_col ? -1 : 1;
+    }
+    // dma(m0, b, full): chunk m0's pieces into buffer b; full (compile time): the chunk is known
+    // to have all R rows.  Called once per chunk with m0 ascending by R from m_lo (the running
+    // row addresses rely on it).
     auto dma = [&](int m0, int b, auto fullc) {
-      const char* rowp = prow;
-      prow += rstep;
-      if (!has_piece) return;
-      if (!decltype(fullc)::value && pr >= m_hi - m0) return;  // row past the segment
-      const int wo = __builtin_amdgcn_readfirstlane(wlo_s[m0 - m_lo + pr]);
-      const int wn = __builtin_amdgcn_readfirstlane(wnum_s[m0 - m_lo + pr]);
-      if (128 * ph + ppar >= wn) return;  // piece wholly past the touched width
-      // the row base is block-uniform: force it into SGPRs (a VGPR base makes hipcc wrap
-      // the DMA in a waterfall loop over the distinct resource values)
-      const uint64_t rb = (uint64_t)(uintptr_t)rowp;
-      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)rb);
-      const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(rb >> 32));
-      const __amdgpu_buffer_rsrc_t rs = make_rsrc((const void*)(uintptr_t)(((uint64_t)hi << 32) | lo), rowbytes);
-      const int col = pcol + psgn * wo;
-      // negative columns wrap to huge unsigned offsets: out of range, zero-filled (slots past
-      // the row's touched width are fetched but never read by a tap: masking them cost more
-      // VALU than the L2 fetch it saved)
-      const unsigned voff = MIRROR ? (unsigned)((col * VBR + mq * MH) * (int)sizeof(T))
-                                   : (unsigned)((col * VB + ppl * PV) * (int)sizeof(T));
-      if (b == 0)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)&win[ppl][pr][pslot],
-                                                 16, voff, 0, 0, 0);
-      else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)&win1[ppl][pr][pslot],
-                                                 16, voff, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < NPW; ++i) {
+        Piece& P = pc[i];
+        const char* rowp = P.prow;
+        P.prow += P.rstep;
+        if (!P.has) continue;
+        if (!decltype(fullc)::value && P.pr >= m_hi - m0) continue;  // row past the segment
+        const int wo = __builtin_amdgcn_readfirstlane(wlo_s[m0 - m_lo + P.pr]);
+        const int wn = __builtin_amdgcn_readfirstlane(wnum_s[m0 - m_lo + P.pr]);
+        if (128 * P.ph + P.ppar >= wn) continue;  // piece wholly past the touched width
+        // the row base is block-uniform: force it into SGPRs (a VGPR base makes hipcc wrap
+        // the DMA in a waterfall loop over the distinct resource values)
+        const uint64_t rb = (uint64_t)(uintptr_t)rowp;
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)rb);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(rb >> 32));
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc((const void*)(uintptr_t)(((uint64_t)hi << 32) | lo), rowbytes);
+        const int col = P.pcol + P.psgn * wo;
+        // negative columns wrap to huge unsigned offsets: out of range, zero-filled (slots past
+        // the row's touched width are fetched but never read by a tap: masking them cost more
+        // VALU than the L2 fetch it saved)
+        const unsigned voff = MIRROR ? (unsigned)((col * VBR + mq * MH) * (int)sizeof(T))
+                                     : (unsigned)((col * VB + P.ppl * PV) * (int)sizeof(T));
+        if (b == 0)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rs, (__attribute__((address_space(3))) void*)&win[P.ppl][P.pr][P.pslot], 16, voff, 0, 0, 0);
+        else
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rs, (__attribute__((address_space(3))) void*)&win1[P.ppl][P.pr][P.pslot], 16, voff, 0, 0, 0);
+      }
     };
     dma(m_lo, 0, std::false_type{});
     __syncthreads();  // (its fence waits for this wave's LDS-DMA: vmcnt(0)) chunk 0 staged
