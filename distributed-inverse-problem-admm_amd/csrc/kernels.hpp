@@ -486,7 +486,7 @@ constexpr int kFgThreads = 64 * kFgG;
 constexpr int kFgWin = ADMM_FG_WIN;    // staged window width (pixels)
 constexpr int kFgSeg = ADMM_FG_SEG;    // row segments (partial sums) per ray
 #ifndef ADMM_FG_DMA_ROWS
-#define ADMM_FG_DMA_ROWS 2  // rows per chunk of the LDS-DMA kernel (4: 34.7 us, 1: 38.0 us at 512^2 vs 32.5)
+#define ADMM_FG_DMA_ROWS 2  // rows per chunk of the LDS-DMA kernel (round 4: 4 rows 50.0 vs 51.2 us at C3, 28.2 vs 27.7 at 8 nodes)
 #endif
 constexpr int kFgHalf = kFgWin / 2;                // slots per parity
 constexpr int kFgPieces = (kFgHalf + 63) / 64;     // 64-slot LDS-DMA pieces per parity half
