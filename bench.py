@@ -40,16 +40,18 @@ predicted_speedup = T_1 / (T_rank + t_exchange), T_1 = the config on one GPU (me
 in the same run); ``per_node_cost_ratio`` = (T_rank / V_rank) / (T_1 / V).  ``--as-rank
 R/W`` with ``--config`` prints one such share as its own line.
 
-Roofline (``roofline``): the dominant kernel is the forward projector's tap kernel
-k_fwdg.  Its average launch duration is measured live with HIP events on the stream it
-runs on; its HBM bytes per launch come from the committed rocprofv3 PMC passes
-(2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md) of the in-solve launches of the same
-workload (TRAFFIC_FILES), so ``frac`` = PMC bytes / live duration / 8 TB/s.
-``compulsory_bytes`` is what one launch must move at least (each node image read once,
-its sinogram written once); ``sample_touch`` is SURVEY.md 8d's per-tap accounting, which
-counts LDS-served taps and so exceeds any memory peak -- it is reported as a reuse
-factor, not a rate.  ``step_hbm`` is the whole step's PMC traffic over the measured step
-time.
+Roofline (``roofline``): the dominant kernel -- of the two projectors, each launched once
+per CG step, the one with the longer in-solve launch (at C3 the back projector
+k_back_mirror in H mode, ahead of the forward taps k_fwdg); both are reported as
+``roofline_back`` and ``roofline_fwd``.  A kernel's average launch duration is measured live
+with HIP events on the stream it runs on, around each of its in-solve launches; its HBM bytes
+per launch come from the committed rocprofv3 PMC passes (2 x FETCH_SIZE + WRITE_SIZE,
+MI355X_MICROARCH.md) of the in-solve launches of the same workload (TRAFFIC_FILES), so
+``frac`` = PMC bytes / live duration / 8 TB/s.  ``compulsory_bytes`` is what one launch must
+move at least; ``lds`` puts the tap reads (LDS-served) against the aggregate ds_read_b128
+rate; ``sample_touch`` is SURVEY.md 8d's per-tap accounting, which counts LDS-served taps
+and so exceeds any memory peak -- a reuse factor, not a rate.  ``step_hbm`` is the whole
+step's PMC traffic over the measured step time.
 
 CPU baseline (``cpu_baseline``): the float64 NumPy/SciPy oracle (oracle/, the port of
 the reference algorithm -- the reference's CVXPY/ODL path cannot run here) doing the
@@ -78,6 +80,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 LDS_PEAK_GBS = 150000.0  # aggregate ds_read_b128 rate, every CU streaming (MI355X_MICROARCH.md, LDS)
 CPU_BASELINE_SECONDS = 8.0  # per-process compute budget of the bounded CPU sample
 XGMI_LINK_GBS, XGMI_LINKS = 153.0, 7  # per direction per link, links per MI355X (task spec)
+RCCL_CALL_US = 50.0  # assumed fixed cost per RCCL call per iteration (launch + handshake), conservative model
 
 
 # BASELINE.json configs[1..4]: image side, total graph nodes, graph, dtype, TV
@@ -262,7 +265,7 @@ def pmc_traffic(workload):
 
 
 STREAMS = 1  # concurrent batch streams per rank (--streams; RankGroups)
-STORED_Z = False  # --stored-z: keep z per edge instead of deriving it (A/B of ABI 7)
+EDGE_STATE = None  # --edge-state stored|derived forces z's form (default: the run's rule, plan.z_is_stored)
 
 
 def setup_run(name, world, rank, local_rank, exchange=True):
@@ -286,7 +289,8 @@ def setup_run(name, world, rank, local_rank, exchange=True):
     sinos = dict(zip(local, make_sinograms([ops[g] for g in local], ph, 0.005, seed=1000 + local[0])))
     Wi, Q = make_precisions(ops)  # one W kernel launch: every node shares the geometry
     rg = RankGroups(ops, G, V_total, world, rank, sinos, Q, RHO, LAM, 10 * LAM, TV_ITERS, CG_ITERS, tv_kind, ph,
-                    keep_x=True, halo=exchange, streams=STREAMS, derive_z=False if STORED_Z else None)
+                    keep_x=True, halo=exchange, streams=STREAMS,
+                    derive_z=None if EDGE_STATE is None else EDGE_STATE == "derived")
     return dict(name=name, n_img=n_img, V_total=V_total, dtype=dtype, tv_kind=tv_kind, geom=geom, plan=rg.plan,
                 rg=rg, nb=rg.batches[0], Wi=Wi, graph=cfg["graph"])
 
@@ -306,8 +310,7 @@ def timed_steps(r, steps, warmup, world, prime=None, markers=False):
         rg.node_update()
         if first and prime is not None:
             prime(rg.batches[0])
-        rg.exchange()
-        rg.consensus()
+        rg.exchange_consensus()  # (rank-internal edges under the halo exchange)
         # the statistics the stop test reads (global table, RCCL all-reduce at N > 1), read
         # back every step into pinned host memory without a per-step host synchronisation --
         # run_admm's pipelined mode (the stop test cannot fire at eps = 0)
@@ -372,9 +375,14 @@ def exchange_model(plan, n_img):
         peers = sum(1 for v in plan.recv.values() if v)
         mode = "p2p"
     links = max(1, min(peers, XGMI_LINKS))
+    calls = 2  # the halo exchange (one all-gather, or one grouped p2p batch) + the statistics all-reduce
+    lat = calls * RCCL_CALL_US * 1e-3
     return {"mode": mode, "bytes_received": recv, "peers": peers, "stats_bytes": stats_bytes,
+            "rccl_calls": calls,
             "ms_direct": 1e3 * (recv + stats_bytes) / (links * XGMI_LINK_GBS * 1e9),
-            "ms_one_link": 1e3 * (recv + stats_bytes) / (XGMI_LINK_GBS * 1e9)}
+            "ms_one_link": 1e3 * (recv + stats_bytes) / (XGMI_LINK_GBS * 1e9),
+            # conservative: every received byte over ONE link, plus a fixed cost per RCCL call
+            "ms_conservative": 1e3 * (recv + stats_bytes) / (XGMI_LINK_GBS * 1e9) + lat}
 
 
 def busiest_rank(name, world):
@@ -421,13 +429,15 @@ def proxy(name, world, t1_ms, V_total, steps, warmup):
     busiest rank's (if different), the exchange, the predicted speedup over one GPU."""
     ranks = sorted({0, busiest_rank(name, world)})
     shares = [time_share(name, world, r, steps, warmup) for r in ranks]
-    worst = max(shares, key=lambda s: s["ms_per_step"] + s["exchange"]["ms_direct"])
+    worst = max(shares, key=lambda s: s["ms_per_step"] + s["exchange"]["ms_conservative"])
+    t_c = worst["ms_per_step"] + worst["exchange"]["ms_conservative"]
     t_d = worst["ms_per_step"] + worst["exchange"]["ms_direct"]
     t_1 = worst["ms_per_step"] + worst["exchange"]["ms_one_link"]
     return {"config": name, "ranks": world, "shares": shares, "T1_ms_per_step": t1_ms,
             "per_node_cost_ratio": (worst["ms_per_step"] / worst["local_nodes"]) / (t1_ms / V_total),
-            "predicted_ms_per_step": t_d, "predicted_speedup": t1_ms / t_d,
-            "predicted_speedup_one_link": t1_ms / t_1}
+            # headline prediction: the conservative exchange (one link + per-call latency)
+            "predicted_ms_per_step": t_c, "predicted_speedup": t1_ms / t_c,
+            "predicted_speedup_one_link": t1_ms / t_1, "predicted_speedup_direct": t1_ms / t_d}
 
 
 def launch_ranks(n: int) -> int:
@@ -465,77 +475,110 @@ def launch_ranks(n: int) -> int:
     return status
 
 
-def forward_roofline(r, workload, fwd_reps):
-    """``roofline`` of the dominant kernel (forward taps) of a bound workload: live HIP-event
-    timing of its in-solve launches, PMC bytes from the committed passes of that workload."""
-    nb, geom, plan = r["nb"], r["geom"], r["plan"]
-    # HIP events around every CG-step forward of one more x-update (after the timed region
-    # and the halo check), each launch right after the CG / TV update that wrote its image, as
-    # in the timed steps -- the figure rocprofv3's in-solve average must agree with;
-    # back-to-back launches, which find the image rows still in L2, are reported beside it
-    fwd_ms = nb.time_forward(in_solve=True)
-    fwd_ms_warm = nb.time_forward(fwd_reps)
-    n_img, dtype = r["n_img"], r["dtype"]
-    a_node = geom.n_angles
-    sbytes = 8 if dtype == "float64" else 4
-    B_A, _, _ = sample_touch_bytes(n_img, a_node, TV_ITERS, CG_ITERS, sbytes)
-    V = nb.V
-    n, m = n_img * n_img, a_node * n_img
-    compulsory = V * n * sbytes + V * m * sbytes  # each node image read once, its sinogram written once
-    as_designed = 2 * V * n * sbytes + 8 * V * m * sbytes  # image + transposed copy, 8 segment partials
-    lds_bytes = sbytes * a_node * n_img * 2 * n_img * V  # m rays x N rows x 2 taps x V samples
-    tr, tr_file = pmc_traffic(workload)
-    tname = "double" if dtype == "float64" else "float"
-    vbv = min(2 * nb.ctx_vb, 32 // sbytes)  # mirror mode's virtual width
-    fwd_traffic = fwd_kernel_traffic(tr, tname, nb.ctx_vb, nb.mirror)
-    fwd_s = fwd_ms * 1e-3
+def back_kernel_traffic(tr, tname, vb, mirror):
+    """PMC bytes per launch of the batch's in-solve back projector (BACK_H = mode 3):
+    k_back_mirror<T, VBV, VBR, 3> in mirror mode, k_back<T, VB, 3, false> otherwise."""
+    if not tr:
+        return None
+    vbv = min(2 * vb, 32 // (8 if tname == "double" else 4))
+    want = f"admm::k_back_mirror<{tname}, {vbv}, {vb}, 3>" if mirror else f"admm::k_back<{tname}, {vb}, 3, false>"
+    return tr["kernels"].get(want, {}).get("hbm_bytes_per_launch")
+
+
+def _roof(kernel, traffic, tr_file, ms, compulsory, lds_bytes, extra=None):
+    """One kernel's roofline entry: PMC bytes per launch / live event-timed in-solve duration
+    against the 8 TB/s HBM peak, compulsory bytes beside it, LDS tap reads against the
+    aggregate ds_read_b128 rate."""
+    s = ms * 1e-3
     roof = {
-        "kernel": (f"k_fwdg<{tname},{vbv},true,{nb.ctx_vb}> (mirror mode: virtual {vbv}-lane images over half "
-                   f"the angles; " if nb.mirror else f"k_fwdg<{tname},{nb.ctx_vb}> (")
-                  + f"Joseph forward projector taps, angle-grouped, 8 row-segment partial sums per ray; {V} nodes "
-                  f"= {-(-V // nb.ctx_vb)} node chunk(s) per launch)",
-        # the angle-group plan the batch bound (admm_fwd_plan_info): 0 = 64-ray chunks,
-        # 1 = aligned per (segment, angle), 2 = aligned per (segment, chunk); 3-5 = clipped
-        "fwd_plan": next((dict(p) for p in nb.fwd_plans() if p["active"]), None),
-        # mirror mode: the batch projects virtual images over half the angles (admm_batch_info)
-        "mirror": nb.mirror,
+        "kernel": kernel,
         "bound": "hbm",
-        "achieved": fwd_traffic / fwd_s / 1e9 if fwd_traffic is not None else None,
+        "achieved": traffic / s / 1e9 if traffic is not None else None,
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
-        "frac": fwd_traffic / fwd_s / 1e9 / HBM_PEAK_GBS if fwd_traffic is not None else None,
-        "traffic": fwd_traffic,
+        "frac": traffic / s / 1e9 / HBM_PEAK_GBS if traffic is not None else None,
+        "traffic": traffic,
         "traffic_source": (f"{tr_file}: rocprofv3 PMC 2 x FETCH_SIZE + WRITE_SIZE per in-solve launch "
-                           "(Infinity-Cache hits included)") if fwd_traffic is not None else None,
-        "avg_launch_ms": fwd_ms,
-        "avg_launch_ms_back_to_back": fwd_ms_warm,
+                           "(Infinity-Cache hits included)") if traffic is not None else None,
+        "avg_launch_ms": ms,
         "compulsory_bytes": compulsory,
-        "compulsory_frac": compulsory / fwd_s / 1e9 / HBM_PEAK_GBS,
-        "as_designed_bytes": as_designed,
-        "traffic_over_compulsory": fwd_traffic / compulsory if fwd_traffic is not None else None,
-        "sample_touch_bytes": B_A * V,
-        "reuse_factor": B_A * V / compulsory,
-        "note": "frac = PMC bytes per launch / live event-timed duration of the in-solve launches (HIP "
-                "events around each CG-step forward of one x-update) / 8 TB/s. compulsory = each "
-                "node image read once + its sinogram written once; as_designed adds the transposed "
-                "image copy (case-A angles) and the 8 segment partials. sample_touch (SURVEY 8d) "
-                "counts every tap as a 4-byte load; taps are LDS reads, so it is a reuse factor, "
-                "not an HBM rate (see DESIGN.md)",
-        # the bound that actually applies on chip: every tap is an LDS read of the staged
-        # window (2 taps x V samples per ray and row), against the measured ds_read_b128 peak
+        "compulsory_frac": compulsory / s / 1e9 / HBM_PEAK_GBS,
+        "traffic_over_compulsory": traffic / compulsory if traffic is not None else None,
+        # the bound that actually applies on chip: every tap is an LDS read of a staged window
         "lds": {
-            "achieved": lds_bytes / fwd_s / 1e9,
+            "achieved": lds_bytes / s / 1e9,
             "peak": LDS_PEAK_GBS,
             "unit": "GB/s",
-            "frac": lds_bytes / fwd_s / 1e9 / LDS_PEAK_GBS,
+            "frac": lds_bytes / s / 1e9 / LDS_PEAK_GBS,
             "bytes_per_launch": lds_bytes,
             "note": "tap reads only (staging writes excluded); peak = MI355X_MICROARCH.md aggregate "
                     "ds_read_b128 rate, all CUs streaming",
         },
     }
+    roof.update(extra or {})
     if roof["frac"] is not None:
         assert roof["frac"] <= 1.0, roof
-    return roof, tr, tr_file
+    return roof
+
+
+def projector_rooflines(r, workload, fwd_reps):
+    """Rooflines of the two projector kernels of a bound workload (each launched once per CG
+    step): live HIP-event timing of their in-solve launches, PMC bytes from the committed
+    passes of that workload.  Returns (dominant, forward, back, traffic, traffic file): the
+    dominant one is the kernel with the larger in-solve time (both run tv x cg times)."""
+    nb, geom = r["nb"], r["geom"]
+    # HIP events around every CG-step launch of one more x-update each (after the timed region
+    # and the halo check), each launch right after the kernel that wrote its input, as in the
+    # timed steps -- the figures rocprofv3's in-solve averages must agree with; back-to-back
+    # forward launches, which find the image rows still in L2, are reported beside them
+    fwd_ms = nb.time_forward(in_solve=True)
+    fwd_ms_warm = nb.time_forward(fwd_reps)
+    back_ms = nb.time_back()
+    n_img, dtype = r["n_img"], r["dtype"]
+    a_node = geom.n_angles
+    sb = 8 if dtype == "float64" else 4
+    B_A, B_At, _ = sample_touch_bytes(n_img, a_node, TV_ITERS, CG_ITERS, sb)
+    V, vb, mirror = nb.V, nb.ctx_vb, nb.mirror
+    n, m = n_img * n_img, a_node * n_img
+    tr, tr_file = pmc_traffic(workload)
+    tname = "double" if dtype == "float64" else "float"
+    vbv = min(2 * vb, 32 // sb)  # mirror mode's virtual width
+    chunks = f"{V} nodes = {-(-V // vb)} node chunk(s) per launch"
+    # forward taps: each node image read once, its sinogram written once (compulsory); the
+    # design adds the transposed image copy (case-A angles) and the 8 segment partials
+    fwd_comp = V * n * sb + V * m * sb
+    fwd = _roof((f"k_fwdg<{tname},{vbv},true,{vb}> (mirror mode: virtual {vbv}-lane images over half the "
+                 f"angles; " if mirror else f"k_fwdg<{tname},{vb}> (")
+                + f"Joseph forward projector taps, angle-grouped, 8 row-segment partial sums per ray; {chunks})",
+                fwd_kernel_traffic(tr, tname, vb, mirror), tr_file, fwd_ms, fwd_comp,
+                sb * a_node * n_img * 2 * n_img * V,  # m rays x N rows x 2 taps x V samples
+                {"fwd_plan": next((dict(p) for p in nb.fwd_plans() if p["active"]), None), "mirror": mirror,
+                 "avg_launch_ms_back_to_back": fwd_ms_warm,
+                 "as_designed_bytes": 2 * V * n * sb + 8 * V * m * sb,
+                 "sample_touch_bytes": B_A * V, "reuse_factor": B_A * V / fwd_comp,
+                 "note": "frac = PMC bytes per launch / live event-timed duration of the in-solve launches "
+                         "(HIP events around each CG-step forward of one x-update) / 8 TB/s. compulsory = "
+                         "each node image read once + its sinogram written once. sample_touch (SURVEY 8d) "
+                         "counts every tap as a load; taps are LDS reads, so it is a reuse factor, not an "
+                         "HBM rate (see DESIGN.md)"})
+    # back projector in H mode (A^T s fused with H p = A^T A p + rho D p + mu K^T K p and the five
+    # CG dot products): compulsory = sinogram, p, D (samples) and r (float64) read once, Hp written
+    back_comp = V * m * sb + 3 * V * n * sb + V * n * 8
+    back = _roof((f"k_back_mirror<{tname},{vbv},{vb},BACK_H> (mirror mode: pixel pairs (i, j), (N-1-i, j) "
+                  f"of the upper half over half the angles; " if mirror else f"k_back<{tname},{vb},BACK_H> (")
+                 + f"pixel-driven Joseph adjoint taps from LDS sinogram windows, fused H epilogue and CG "
+                 f"dot partials; {chunks})",
+                 back_kernel_traffic(tr, tname, vb, mirror), tr_file, back_ms, back_comp,
+                 sb * n * a_node * 2 * V,  # n pixels x a angles x 2 taps x V samples
+                 {"mirror": mirror, "sample_touch_bytes": B_At * V,
+                  "note": "frac = PMC bytes per launch / live event-timed duration of the in-solve launches "
+                          "(HIP events around each CG-step back projection of one x-update) / 8 TB/s. "
+                          "compulsory = sinogram, p, D read once as samples, r (float64) read once, Hp "
+                          "written once"})
+    dom = dict(back if back_ms >= fwd_ms else fwd)
+    dom["dominant_by"] = (f"in-solve time per CG step: back {back_ms * 1e3:.1f} us vs forward taps "
+                          f"{fwd_ms * 1e3:.1f} us (one launch each per CG step)")
+    return dom, fwd, back, tr, tr_file
 
 
 def describe(r, world):
@@ -568,7 +611,7 @@ def leg(name, world, rank, local_rank, steps, warmup):
 
 
 def main():
-    global STREAMS, STORED_Z
+    global STREAMS, EDGE_STATE
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -592,15 +635,17 @@ def main():
     ap.add_argument("--streams", type=int, default=STREAMS,
                     help="split each rank's nodes into up to this many batches (>= 8 float32 / 4 float64 "
                          "nodes each) whose kernels run concurrently on their own streams")
-    ap.add_argument("--stored-z", action="store_true",
-                    help="keep z per edge (the pre-ABI-7 edge state) instead of deriving it: A/B")
+    ap.add_argument("--edge-state", choices=("auto", "stored", "derived"), default="auto",
+                    help="z kept per edge or derived from the endpoint images (ABI 7); auto = the run's "
+                         "rule (stored wherever the edge state fits, admm_hip/plan.py z_is_stored)")
+    ap.add_argument("--stored-z", action="store_true", help="= --edge-state stored")
     ap.add_argument("--headline-only", action="store_true",
                     help="only the headline workload (no weak8, strong or proxy legs): rocprofv3 runs")
     args = ap.parse_args()
     if args.headline_only:
         args.strong, args.proxy = "none", "none"
     STREAMS = max(1, args.streams)
-    STORED_Z = bool(args.stored_z)
+    EDGE_STATE = "stored" if args.stored_z else (None if args.edge_state == "auto" else args.edge_state)
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
     if args.as_rank is not None and args.config is None:
@@ -661,7 +706,7 @@ def main():
     n_img, V_total, dtype = r["n_img"], r["V_total"], r["dtype"]
     value = V_total * args.steps / el
     ms_per_step = 1e3 * el / args.steps
-    roof, tr, tr_file = forward_roofline(r, workload, args.fwd_reps)
+    roof, roof_fwd, roof_back, tr, tr_file = projector_rooflines(r, workload, args.fwd_reps)
     headline_fixed = workload in CONFIGS  # a fixed-size config (C3 headline, --config)
     result = {
         "metric": "ADMM node-updates/sec (whole node), 512² phantom; rel-Fro vs CPU ref",
@@ -685,6 +730,8 @@ def main():
             "batch_streams": len(r["rg"].streams) if r["rg"].streams else 1,
         },
         "roofline": roof,
+        "roofline_fwd": roof_fwd,
+        "roofline_back": roof_back,
     }
     if xcheck is not None:
         result["exchange_check"] = dict(xcheck, backend=backend, mode=r["rg"].halo.mode,
@@ -727,9 +774,11 @@ def main():
             px[f"{name}@{W}"] = proxy(name, W, t, V, args.proxy_steps, 1)
         result["proxy_8gpu"] = dict(
             px, model=f"T_rank = rank's share timed on this GPU (halo rows fixed); exchange = bytes received "
-                      f"(float64 images + statistics) over xGMI, direct = min(peers, {XGMI_LINKS}) links x "
-                      f"{XGMI_LINK_GBS:.0f} GB/s, one_link = a single link; predicted_speedup = T_1 / "
-                      f"(T_rank + exchange_direct); the exchange is not overlapped with compute")
+                      f"(float64 images + statistics) over xGMI at {XGMI_LINK_GBS:.0f} GB/s per link: "
+                      f"conservative = one link + {RCCL_CALL_US:.0f} us per RCCL call (assumed; 2 calls per "
+                      f"iteration), one_link = one link, direct = min(peers, {XGMI_LINKS}) links; "
+                      f"predicted_speedup = T_1 / (T_rank + exchange_conservative); only the rank-internal "
+                      f"edge updates overlap the all-gather (not priced)")
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

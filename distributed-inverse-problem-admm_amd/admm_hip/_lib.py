@@ -20,7 +20,7 @@ ADMM_TV_ANISO = 1
 ADMM_FUSE_MIDPOINT = 0
 ADMM_FUSE_WEIGHTED = 1
 ADMM_BATCH_KEEP_X = 1  # admm_batch.flags: x_ext local rows written only by admm_node_update
-ABI_VERSION = 8
+ABI_VERSION = 9
 ADMM_MASK_KNN = 0
 ADMM_MASK_MST = 1
 ADMM_MASK_CHAIN = 2
@@ -109,6 +109,8 @@ SYMBOLS = {
     "admm_consensus": [C.c_void_p, C.c_void_p],
     "admm_time_forward": [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_double)],
     "admm_batch_info": [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)],
+    "admm_time_back": [C.c_void_p, C.c_void_p, C.POINTER(C.c_double)],
+    "admm_consensus_range": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p],
     "admm_fwd_plan_info": [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
                            C.POINTER(C.c_double), C.POINTER(C.c_int)],
     "admm_pixel_masks": [C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_void_p,

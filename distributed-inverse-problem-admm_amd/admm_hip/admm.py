@@ -87,8 +87,10 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
              cg_iters=5, tv_kind="iso", group=None, return_tensors=False, timing=None,
              write_params=True, fusion="midpoint", inner_tol=None, max_inner_updates=10,
              inner_chunks=None, chunk_snapshot_dir=None, chunk_save_every=1, inspect=None,
-             pipeline=None, streams=1):
-    """``inner_chunks``: split each x-update into warm-started solves of these round counts
+             pipeline=None, streams=1, edge_state=None):
+    """``edge_state``: "stored" / "derived" z (None: the run's rule, plan.z_is_stored --
+    stored wherever it fits; ADMM_EDGE_STATE in the environment forces it too).
+``inner_chunks``: split each x-update into warm-started solves of these round counts
     (block_6_admm_loop.py:14-69 chunked SCS); ``chunk_snapshot_dir`` then receives that
     file's per-chunk snapshots (``_chunk_snapshot``) every ``chunk_save_every`` chunks.
     ``inspect(rg)``: called with the rank's device state (groups.RankGroups) after the loop
@@ -127,7 +129,8 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
         snapshot_every = max(1, max_iters // snapshot_div)  # _ver2:31-32
     rg = RankGroups(A_dense_list, G, V_total, world, rank, sinograms, Qij_diag_fn, rho, lam_tv, mu,
                     tv_iters, cg_iters, tv_kind, phantom_true, fusion=fusion, Wi_list=Wi_list,
-                    keep_x=inner_tol is None, group=group, streams=streams)  # this loop never writes x itself
+                    keep_x=inner_tol is None, group=group, streams=streams,  # this loop never writes x itself
+                    derive_z=None if edge_state is None else {"stored": False, "derived": True}[edge_state])
     # (masked re-solves of the tolerance mode restore x rows, so that mode re-projects x)
     plan = rg.plan
     if world > 1:
@@ -168,8 +171,7 @@ def run_admm(A_dense_list, sinograms, G, Wi_list, Qij_diag_fn, N, lam_tv=0.01, r
             for nb in rg.batches:
                 rows = [plan.local_nodes.index(g) for g in nb.plan.local_nodes]
                 eps_used[rows], n_upd[rows] = _solve_to_reference_tolerance(nb, et, max_inner_updates)
-        rg.exchange()
-        rg.consensus()
+        rg.exchange_consensus()  # (rank-internal edges under the halo exchange)
         iters_done = k + 1
         if pipelined:
             flat = rg.stats_device()

@@ -37,6 +37,11 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None,
     if not force and out is None and not needs_build():
         return OUT
     arch = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
+    if arch != "gfx950":
+        # the kernels are written for CDNA4: 160 KiB of LDS per workgroup (k_consensus_derived<128>
+        # declares 128 KiB, the back projector's windows + DIAG tile ~80 KiB), v_permlane32/16_swap
+        # and LDS-DMA widths of gfx950
+        raise RuntimeError(f"libadmm_tomo targets gfx950 (MI355X) only; PYTORCH_ROCM_ARCH={arch!r}")
     tmp = target + ".tmp"
     dflags = [f"-D{k}={v}" for k, v in (defines or {}).items()]
     # -ffp-contract=off: no compiler-formed fmas.  Contraction is decided per template

@@ -61,20 +61,24 @@ class HaloExchange:
         self.V = V
 
     def run(self) -> None:
+        self.finish(self.start())
+
+    def start(self):
+        """Issue the exchange (asynchronous collectives: RCCL runs them on its own stream after
+        the work already enqueued on the current one); ``finish`` lands the halo rows.  Work
+        enqueued on the current stream between the two -- kernels that read only the local rows
+        -- runs while the images are in flight."""
         if not self.active:
-            return
+            return None
         p = self.plan
         if self.mode == "allgather":
             self.sendbuf[: self.V].copy_(self.x[: self.V])
             if self.stage:
                 full = self.full.cpu()
-                dist.all_gather_into_tensor(full, self.sendbuf.cpu(), group=self.group)
-                self.full.copy_(full)
-            else:
-                dist.all_gather_into_tensor(self.full, self.sendbuf, group=self.group)
-            if len(p.halo_nodes):
-                self.x[self.V:].copy_(self.full.index_select(0, self.halo_idx))
-            return
+                return ("ag", dist.all_gather_into_tensor(full, self.sendbuf.cpu(), group=self.group,
+                                                          async_op=True), full)
+            return ("ag", dist.all_gather_into_tensor(self.full, self.sendbuf, group=self.group, async_op=True),
+                    None)
         ops, landing = [], []
         for peer, rows, buf in self.sends:
             torch.index_select(self.x, 0, rows, out=buf)
@@ -86,10 +90,22 @@ class HaloExchange:
                 landing.append((dst, host))
                 dst = host
             ops.append(dist.P2POp(dist.irecv, dst, peer, group=self.group))
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
-        for dst, host in landing:
+        return ("p2p", dist.batch_isend_irecv(ops) if ops else [], landing)
+
+    def finish(self, h) -> None:
+        if h is None:
+            return
+        kind, work, extra = h
+        if kind == "ag":
+            work.wait()
+            if extra is not None:
+                self.full.copy_(extra)
+            if len(self.plan.halo_nodes):
+                self.x[self.V:].copy_(self.full.index_select(0, self.halo_idx))
+            return
+        for req in work:
+            req.wait()
+        for dst, host in extra:
             dst.copy_(host)
 
 

@@ -23,10 +23,15 @@ operators were equal.
 """
 from __future__ import annotations
 
+import os
+import warnings
+
 import torch
 
 from .exchange import HaloExchange, assemble_stats_device, assemble_stats_parts, gather_images_parts
-from .plan import ShardPlan, make_plan, make_subset_plan
+import torch.distributed as dist
+
+from .plan import STORED_Z_HBM_FRACTION, ShardPlan, make_plan, make_subset_plan, z_is_stored
 from .solver import NodeBatch
 
 
@@ -49,6 +54,84 @@ def max_batch_nodes(geom) -> int:
     return cap - cap % 8 if cap >= 8 else max(1, cap)
 
 
+def rank_batches(A_list, plan: ShardPlan, streams: int = 1):
+    """The device batches of one rank: [(batch key, its global nodes)] in batch order.  Nodes
+    are grouped by operator key; a group larger than one batch may hold is split into
+    consecutive cap-sized chunks -- not near-equal: every edge between two batches is stored
+    (and updated) by both, and for a dense graph the cross edges |A| x |B| are fewest for the
+    most unequal split (C5 on one GPU as 56 + 8 stores 2464 edges, as 32 + 32 it would store
+    3040: +36 GB of float64 edge state); at 2048^2 an 8-node batch is two 4-node chunks of 1816
+    forward blocks each, so the small batch does not idle the GPU.  ``streams`` > 1: every group
+    of at least 2 x SPLIT_MIN nodes is further split into up to that many near-equal
+    consecutive parts of >= SPLIT_MIN nodes (RankGroups' concurrent batches)."""
+    keys, members = [], {}
+    for g in plan.local_nodes:
+        k = operator_key(A_list[g])
+        if k not in members:
+            keys.append(k)
+            members[k] = []
+        members[k].append(g)
+    split = []
+    for k in keys:
+        cap = max_batch_nodes(k[0])
+        nodes = members.pop(k)
+        for c0 in range(0, len(nodes), cap):
+            split.append((k, c0))
+            members[(k, c0)] = nodes[c0:c0 + cap]
+    keys = split
+    if streams > 1:
+        split = []
+        for k in keys:
+            nodes = members.pop(k)
+            parts = max(1, min(streams, len(nodes) // SPLIT_MIN[k[0][1]]))
+            c0 = 0
+            for q in range(parts):
+                sz = len(nodes) // parts + (1 if q < len(nodes) % parts else 0)
+                split.append((k[0], (k[1], q)))  # (operator key, batch tag)
+                members[(k[0], (k[1], q))] = nodes[c0:c0 + sz]
+                c0 += sz
+        keys = split
+    return [(k, members[k]) for k in keys]
+
+
+def stored_edges_per_rank(A_list, G, V_total: int, world: int, streams: int = 1) -> list[int]:
+    """Stored edge slots of every rank of a ``world``-rank run, summed over each rank's device
+    batches (rank_batches) -- what the stored-z rule (plan.z_is_stored) weighs."""
+    out = []
+    for r in range(world):
+        pr = make_plan(G, V_total, world, r)
+        if not pr.local_nodes:
+            out.append(0)
+            continue
+        bs = rank_batches(A_list, pr, streams)
+        if len(bs) == 1:
+            out.append(len(pr.stored_edges))
+        else:
+            out.append(sum(len(make_subset_plan(G, V_total, nodes, world, r, pr.ranges, pr.edges).stored_edges)
+                           for _, nodes in bs))
+    return out
+
+
+def min_over_ranks(value: int, world: int, group=None, device=None) -> int:
+    """``value`` reduced to its minimum over the ranks of a distributed run (one all-reduce;
+    gloo reduces a host tensor, RCCL a tensor on ``device``); the value itself otherwise."""
+    if world > 1 and dist.is_available() and dist.is_initialized():
+        gloo = dist.get_backend(group) == "gloo"
+        t = torch.tensor([int(value)], dtype=torch.int64,
+                         device="cpu" if gloo or device is None else torch.device("cuda", device))
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+        return int(t.item())
+    return int(value)
+
+
+def run_hbm_bytes(device, world: int, group=None, collective: bool = True) -> int:
+    """HBM of the run's devices: this device's total memory, the minimum over ranks when the run
+    is distributed (one all-reduce at setup), so a rule weighed against it is identical on
+    every rank even if the devices differ."""
+    hbm = int(torch.cuda.get_device_properties(device).total_memory)
+    return min_over_ranks(hbm, world, group, device) if collective else hbm
+
+
 class RankGroups:
     def __init__(self, A_list, G, V_total: int, world: int, rank: int, sinograms, Qij_diag_fn,
                  rho, lam, mu, tv_iters, cg_iters, tv_kind, phantom, fusion="midpoint", Wi_list=None,
@@ -59,45 +142,40 @@ class RankGroups:
         batches whose x-updates (and edge updates) run concurrently on their own HIP streams,
         so one batch's kernels fill the other's dependent-launch gaps and kernel tails; each
         batch keeps a full node-interleave width (SPLIT_MIN nodes), and the run is bitwise the
-        one-batch run (the batch split never changes a node's arithmetic)."""
+        one-batch run (the batch split never changes a node's arithmetic).
+        ``derive_z`` None: the run's one edge-state rule (plan.z_is_stored over every rank's
+        stored edges) unless ADMM_EDGE_STATE=stored|derived forces it; True / False force
+        derived / stored z."""
         self.plan: ShardPlan = make_plan(G, V_total, world, rank)
         if not self.plan.local_nodes:
             raise ValueError(f"rank {rank} owns no graph nodes ({V_total} nodes over {world} ranks)")
         self.world = world
         self.group = group
-        keys, members = [], {}
-        for g in self.plan.local_nodes:
-            k = operator_key(A_list[g])
-            if k not in members:
-                keys.append(k)
-                members[k] = []
-            members[k].append(g)
-        # groups larger than one batch may hold are split into consecutive cap-sized chunks.
-        # Not near-equal: every edge between two batches is stored (and updated) by both, and
-        # for a dense graph the cross edges |A| x |B| are fewest for the most unequal split --
-        # C5 on one GPU as 56 + 8 stores 2464 edges, as 32 + 32 it would store 3040 (+36 GB of
-        # float64 edge state); at 2048^2 an 8-node batch is two 4-node chunks of 1816 forward
-        # blocks each, so the small batch does not idle the GPU
-        split = []
-        for k in keys:
-            cap = max_batch_nodes(k[0])
-            nodes = members.pop(k)
-            for c0 in range(0, len(nodes), cap):
-                split.append((k, c0))
-                members[(k, c0)] = nodes[c0:c0 + cap]
-        keys = split
-        if streams > 1:  # concurrent batches: near-equal consecutive parts of >= SPLIT_MIN nodes
-            split = []
-            for k in keys:
-                nodes = members.pop(k)
-                parts = max(1, min(streams, len(nodes) // SPLIT_MIN[k[0][1]]))
-                c0 = 0
-                for q in range(parts):
-                    sz = len(nodes) // parts + (1 if q < len(nodes) % parts else 0)
-                    split.append((k[0], (k[1], q)))  # (operator key, batch tag)
-                    members[(k[0], (k[1], q))] = nodes[c0:c0 + sz]
-                    c0 += sz
-            keys = split
+        dev0 = A_list[self.plan.local_nodes[0]].device
+        n0 = A_list[self.plan.local_nodes[0]].geom.n
+        hbm = run_hbm_bytes(dev0, world, group, collective=halo)
+        if streams > 1:
+            # a stream split stores every cross-batch edge twice (y, and z when stored): the
+            # split is dropped -- on every rank alike, from the busiest rank's extra slots -- when
+            # that extra edge state would exceed the stored-z rule's HBM fraction (ADVICE r4)
+            extra = max(a - b for a, b in zip(stored_edges_per_rank(A_list, G, V_total, world, streams),
+                                              stored_edges_per_rank(A_list, G, V_total, world, 1)))
+            if extra * n0 * 16 > STORED_Z_HBM_FRACTION * hbm:
+                warnings.warn(f"streams={streams} would store {extra} more edge slots on the busiest rank "
+                              f"({extra * n0 * 16 / 2**30:.1f} GiB of float64 edge state): running one batch "
+                              f"stream", RuntimeWarning)
+                streams = 1
+        self.streams_requested = streams
+        bs = rank_batches(A_list, self.plan, streams)
+        keys = [k for k, _ in bs]
+        members = dict(bs)
+        self.fusion = fusion
+        forced = os.environ.get("ADMM_EDGE_STATE", "")
+        if derive_z is None and forced in ("stored", "derived"):
+            derive_z = forced == "derived"
+        if derive_z is None and fusion == "midpoint":
+            derive_z = not z_is_stored(stored_edges_per_rank(A_list, G, V_total, world, streams), n0, hbm, fusion)
+        self.derive_z = bool(derive_z) if derive_z is not None else False
         devices = {k[0][2] for k in keys}
         if len(devices) > 1:
             raise ValueError("a rank's operators must all live on one device (got "
@@ -112,7 +190,7 @@ class RankGroups:
             geom, dtype, device = k[0]
             self.batches.append(NodeBatch(geom, dtype, gp, sinograms, Qij_diag_fn, rho, lam, mu, tv_iters,
                                           cg_iters, tv_kind, phantom, device, fusion=fusion, Wi_list=Wi_list,
-                                          keep_x=keep_x, derive_z=derive_z))
+                                          keep_x=keep_x, derive_z=self.derive_z))
         self.device = self.batches[0].dev
         if len(self.batches) == 1:
             self.x_rank = self.batches[0].x_ext
@@ -170,6 +248,31 @@ class RankGroups:
 
     def consensus(self) -> None:
         self._concurrent(lambda nb: nb.consensus())
+
+    @property
+    def overlaps_exchange(self) -> bool:
+        """exchange_consensus can run the rank-internal edge updates under the halo exchange:
+        one batch, stored z, midpoint fusion, an inter-rank exchange, and internal edges."""
+        if self.halo is None or not self.halo.active or not self.single:
+            return False
+        nb = self.batches[0]
+        return nb.z is not None and nb.fusion == "midpoint" and nb.plan.n_internal > 0
+
+    def exchange_consensus(self) -> None:
+        """``exchange()`` then ``consensus()``, with the edges whose endpoints are both local
+        (stored slots [0, n_internal), x_ext rows < V) updated while the halo images are in
+        flight: the exchange is issued asynchronously (RCCL on its own stream), those edges run
+        on the current stream, then the halo rows land and the remaining edges run.  The same
+        per-edge kernels and statistics as the serial order, bitwise."""
+        if not self.overlaps_exchange or os.environ.get("ADMM_EXCHANGE_OVERLAP", "1") == "0":
+            self.exchange()
+            self.consensus()
+            return
+        nb = self.batches[0]
+        h = self.halo.start()
+        nb.consensus_range(0, nb.plan.n_internal, nb.V)
+        self.halo.finish(h)
+        nb.consensus_range(nb.plan.n_internal, len(nb.plan.stored_edges), nb.plan.n_xext)
 
     def stats(self, extra=None):
         """Global node / edge statistics; ``extra`` (rank-local [V, k] numpy, rows in

@@ -52,6 +52,7 @@ class ShardPlan:
     edge_a_row: list = field(default_factory=list)
     edge_b_row: list = field(default_factory=list)
     owned_edge: list = field(default_factory=list)  # bool per stored edge
+    n_internal: int = 0  # stored slots [0, n_internal): both endpoints local (x_ext rows < V)
     inc_off: list = field(default_factory=list)
     inc_edge: list = field(default_factory=list)    # stored-edge slot
     inc_nbr: list = field(default_factory=list)     # neighbour global id (for Qij_diag_fn)
@@ -128,14 +129,21 @@ def make_subset_plan(G, V_total: int, nodes, world: int = 1, rank: int = 0, rang
     P.halo_nodes = sorted(halo)
     for r, g in enumerate(P.local_nodes + P.halo_nodes):
         P.xrow[g] = r
+    # stored edge slots: the set's internal edges (both endpoints local, x_ext rows < V) first,
+    # then the edges to halo nodes, each in G.edges() order -- so the internal ones can be
+    # updated while the halo exchange is still writing rows >= V (admm_consensus_range); the
+    # per-edge arithmetic does not depend on the slot
+    internal = [ge for ge, (a, b) in enumerate(edges) if a in local and b in local]
+    boundary = [ge for ge, (a, b) in enumerate(edges) if (a in local) != (b in local)]
+    P.n_internal = len(internal)
     eidx = {}
-    for ge, (a, b) in enumerate(edges):
-        if a in local or b in local:
-            eidx[ge] = len(P.stored_edges)
-            P.stored_edges.append(ge)
-            P.edge_a_row.append(P.xrow[a])
-            P.edge_b_row.append(P.xrow[b])
-            P.owned_edge.append(a in local)
+    for ge in internal + boundary:
+        a, b = edges[ge]
+        eidx[ge] = len(P.stored_edges)
+        P.stored_edges.append(ge)
+        P.edge_a_row.append(P.xrow[a])
+        P.edge_b_row.append(P.xrow[b])
+        P.owned_edge.append(a in local)
     edge_of = {e: ge for ge, e in enumerate(edges)}
     P.inc_off = [0]
     for g in P.local_nodes:
@@ -169,3 +177,36 @@ def make_plan(G, V_total: int, world: int = 1, rank: int = 0) -> ShardPlan:
                 need.add(b)
         P.send[peer] = sorted(need)
     return P
+
+
+# --------------------------------------------------------------------------------------
+# Edge-state rule: stored z or z derived from x_prev (ABI 7)
+# --------------------------------------------------------------------------------------
+# Fraction of a GPU's HBM the float64 edge state of its busiest rank may take with z stored
+# (y and z: two rows of n pixels per stored edge slot).  Stored z is the faster edge state
+# wherever it fits (C4 rank 3 of 8: 8.67 vs 8.98 ms per step; C5 rank 0 of 8: 143 vs 154 ms;
+# profiles/r4_shares_derived_vs_stored_z.txt): the gather / DIAG / consensus read one z row per
+# incidence instead of the two endpoint rows of x_prev.  Derived z halves the edge state, so it
+# is kept for graphs whose stored state would not fit.  Every BASELINE config fits at every GPU
+# count; the fullest is C5 on one GPU: 2464 stored edges x 2 x 33.5 MB = 165 GB against
+# 0.6 x 288 GB = 173 GB, leaving ~70 GB for the node state and scratch (~55 GB).
+STORED_Z_HBM_FRACTION = 0.6
+
+
+def stored_edge_state_bytes(stored_edges_per_rank, n: int) -> int:
+    """Bytes of the float64 edge state (y and z, one row of n pixels each per stored edge slot)
+    on the busiest rank; ``stored_edges_per_rank``: every rank's stored edge slots, summed over
+    its device batches (an edge between two batches of one rank is stored by both)."""
+    return max(stored_edges_per_rank) * n * 8 * 2
+
+
+def z_is_stored(stored_edges_per_rank, n: int, hbm_bytes: int, fusion: str = "midpoint",
+                fraction: float = STORED_Z_HBM_FRACTION) -> bool:
+    """The one edge-state rule of a run: stored z iff the busiest rank's y and z rows fit in
+    ``fraction`` of ``hbm_bytes`` (weighted fusion always stores z).  A function of the whole
+    run -- every rank's stored edges, the image size and the devices' HBM -- so every rank gets
+    the same answer: derived and stored z differ in the last bits, and an edge stored on two
+    ranks (or two batches) must be updated bitwise identically at both ends."""
+    if fusion != "midpoint":
+        return True
+    return stored_edge_state_bytes(stored_edges_per_rank, n) <= fraction * hbm_bytes

@@ -23,7 +23,7 @@ import torch
 
 from . import _lib
 from .geometry import ParallelBeamGeometry, RayTransform, current_stream_handle, _Ctx
-from .plan import ShardPlan
+from .plan import ShardPlan, z_is_stored
 
 
 def _as_f64_tensor(v, n: int, dev) -> torch.Tensor:
@@ -44,10 +44,12 @@ class NodeBatch:
                  Qij_diag_fn, rho: float, lam: float, mu: float, tv_iters: int = 10,
                  cg_iters: int = 5, tv_kind: str = "iso", phantom=None, device: int = 0,
                  fusion: str = "midpoint", Wi_list=None, keep_x: bool = False, derive_z: bool | None = None):
-        """``derive_z`` (default: midpoint fusion): z_ij is not stored but derived from the
-        endpoint images of the last consensus (``x_prev``, one row per x_ext row; ABI 7) --
-        bitwise the same z.  block_5's drop-in, which injects arbitrary targets v_ij through z,
-        keeps it stored (``derive_z=False``)."""
+        """``derive_z``: z_ij is not stored but derived from the endpoint images of the last
+        consensus (``x_prev``, one row per x_ext row; ABI 7; midpoint fusion only).  None: the
+        edge-state rule (plan.z_is_stored) on this batch alone -- stored z, the faster form,
+        unless its rows would exceed the rule's share of HBM; RankGroups passes the run's one
+        global decision instead.  block_5's drop-in, which injects arbitrary targets v_ij through
+        z, keeps it stored (``derive_z=False``)."""
         self.lib = _lib.load()
         self.geom = geom
         self.plan = plan
@@ -108,7 +110,8 @@ class NodeBatch:
         if fusion not in ("midpoint", "weighted"):
             raise ValueError("fusion must be 'midpoint' or 'weighted'")
         if derive_z is None:
-            derive_z = fusion == "midpoint"
+            hbm = int(torch.cuda.get_device_properties(dev).total_memory)
+            derive_z = not z_is_stored([E], n, hbm, fusion)
         if derive_z and fusion != "midpoint":
             raise ValueError("derived z needs midpoint fusion")
         self.derive_z = bool(derive_z)
@@ -216,6 +219,14 @@ class NodeBatch:
         if self.plan.stored_edges:
             _lib.check(self.lib.admm_consensus(self.ctx.h, C.c_void_p(self._s())), "admm_consensus")
 
+    def consensus_range(self, e0: int, e1: int, rows: int) -> None:
+        """Edge updates of stored slots [e0, e1) only, whose endpoints lie in x_ext rows [0, rows)
+        (stored z, midpoint fusion; admm_consensus_range, ABI 9): the same per-edge results and
+        statistics as ``consensus``."""
+        if e1 > e0:
+            _lib.check(self.lib.admm_consensus_range(self.ctx.h, int(e0), int(e1), int(rows), C.c_void_p(self._s())),
+                       "admm_consensus_range")
+
     def marker(self) -> None:
         """One k_tv_grad launch (never part of an x-update or consensus): delimits the
         bench's timed steps in rocprofv3 PMC traces (scripts/traffic_summary.py)."""
@@ -232,6 +243,13 @@ class NodeBatch:
         ms = C.c_double()
         _lib.check(self.lib.admm_time_forward(self.ctx.h, reps, int(in_solve), C.c_void_p(self._s()), C.byref(ms)),
                    "admm_time_forward")
+        return ms.value
+
+    def time_back(self) -> float:
+        """Average in-solve back projector launch (ms; k_back / k_back_mirror in H mode): every
+        CG step of one directly enqueued x-update (admm_time_back, ABI 9; the state advances)."""
+        ms = C.c_double()
+        _lib.check(self.lib.admm_time_back(self.ctx.h, C.c_void_p(self._s()), C.byref(ms)), "admm_time_back")
         return ms.value
 
     def fwd_plans(self) -> list[dict]:

@@ -153,6 +153,7 @@ struct admm_ctx {
   // directly enqueued x-update (null outside that measurement)
   std::vector<hipEvent_t>* tf_ev = nullptr;
   size_t tf_next = 0;
+  int tf_kind = 0;  // what the in-solve events bracket: 0 forward taps, 1 back projector (BACK_H)
   bool ats_valid = false;  // ats matches x_ext's local rows
   hipGraph_t g_update_reuse = nullptr;
   hipGraphExec_t x_update_reuse = nullptr;
@@ -435,7 +436,7 @@ int launch_fwd_batch(admm_ctx* C, const T* img, const T* imgT, T* sino, const T*
                      hipStream_t s, bool timed = false) {
   // timed (admm_time_forward in_solve): HIP events right before and after the tap kernel
   hipEvent_t* ev = nullptr;
-  if (timed && C->tf_ev && C->tf_next + 2 <= C->tf_ev->size()) {
+  if (timed && C->tf_ev && C->tf_kind == 0 && C->tf_next + 2 <= C->tf_ev->size()) {
     ev = C->tf_ev->data() + C->tf_next;
     C->tf_next += 2;
     HIPCHK(hipEventRecord(ev[0], s));
@@ -631,7 +632,15 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 
       a.rho = B.rho;
       a.lam = B.lam;
       a.mu = B.mu;
+      // (admm_time_back: events right before and after each in-solve back projection)
+      hipEvent_t* bev = nullptr;
+      if (C->tf_ev && C->tf_kind == 1 && C->tf_next + 2 <= C->tf_ev->size()) {
+        bev = C->tf_ev->data() + C->tf_next;
+        C->tf_next += 2;
+        HIPCHK(hipEventRecord(bev[0], s));
+      }
       RET((launch_back<T, VB, BACK_H>(C, a, V, s)));
+      if (bev) HIPCHK(hipEventRecord(bev[1], s));
       RET(launch_reduce((double*)C->partH.p, 5 * V, Pb, rk, 1, 1, 0, s));
       if (kk + 1 < K) {
         if (F == 2)
@@ -722,6 +731,38 @@ int enqueue_update_any(admm_ctx* C, hipStream_t s, bool reuse = false, int round
 // rows of the derived consensus' LDS tile (0: more x_ext rows than any tile: direct kernel)
 int cons_rows(int n_xext) { return n_xext <= 16 ? 16 : n_xext <= 64 ? 64 : n_xext <= 128 ? 128 : 0; }
 
+// stored-z midpoint consensus of edge slots [e0, e1) whose endpoints lie in x_ext rows [0, R)
+// (k_consensus_stored; the LDS tile when R fits one, the same results otherwise)
+int enqueue_consensus_stored(admm_ctx* C, int e0, int e1, int R, hipStream_t s) {
+  const admm_batch& B = C->b;
+  if (e1 <= e0) return ADMM_OK;
+  const int npix = C->npix;
+  const dim3 g((npix + kConsPix - 1) / kConsPix);
+  double* part = (double*)C->partE.p;
+  switch (cons_rows(R)) {
+    case 16:
+      hipLaunchKernelGGL(k_consensus_stored<16>, g, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.edge_a, B.edge_b, part,
+                         npix, R, e0, e1);
+      break;
+    case 64:
+      hipLaunchKernelGGL(k_consensus_stored<64>, g, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.edge_a, B.edge_b, part,
+                         npix, R, e0, e1);
+      break;
+    case 128:
+      hipLaunchKernelGGL(k_consensus_stored<128>, g, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.edge_a, B.edge_b, part,
+                         npix, R, e0, e1);
+      break;
+    default:
+      hipLaunchKernelGGL(k_consensus_stored<0>, g, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.edge_a, B.edge_b, part,
+                         npix, R, e0, e1);
+  }
+  CHECK_LAUNCH();
+  // rows 3 e0 .. 3 e1 - 1 of the partials -> edge_stats rows e0 .. e1 - 1
+  RET(launch_reduce(part + (size_t)3 * e0 * C->P_edge, 3 * (e1 - e0), C->P_edge, B.edge_stats + (size_t)3 * e0, 1, 1,
+                    0, s));
+  return ADMM_OK;
+}
+
 int enqueue_consensus(admm_ctx* C, hipStream_t s) {
   const admm_batch& B = C->b;
   if (B.n_edges == 0) return ADMM_OK;
@@ -755,13 +796,10 @@ int enqueue_consensus(admm_ctx* C, hipStream_t s) {
     RET(launch_reduce(part, 3 * B.n_edges, C->P_edge, B.edge_stats, 1, 1, 0, s));
     return ADMM_OK;
   }
+  if (B.fusion == ADMM_FUSE_MIDPOINT) return enqueue_consensus_stored(C, 0, B.n_edges, B.n_xext, s);
   dim3 grid((npix + kBlock * 4 - 1) / (kBlock * 4), B.n_edges);
-  if (B.fusion == ADMM_FUSE_WEIGHTED)
-    hipLaunchKernelGGL(k_consensus<true>, grid, dim3(kBlock), 0, s, B.x_ext, B.y, B.y_b, B.z, B.w, B.edge_a,
-                       B.edge_b, (double*)C->partE.p, npix);
-  else
-    hipLaunchKernelGGL(k_consensus<false>, grid, dim3(kBlock), 0, s, B.x_ext, B.y, nullptr, B.z, nullptr,
-                       B.edge_a, B.edge_b, (double*)C->partE.p, npix);
+  hipLaunchKernelGGL(k_consensus<true>, grid, dim3(kBlock), 0, s, B.x_ext, B.y, B.y_b, B.z, B.w, B.edge_a,
+                     B.edge_b, (double*)C->partE.p, npix);
   CHECK_LAUNCH();
   RET(launch_reduce((double*)C->partE.p, 3 * B.n_edges, C->P_edge, B.edge_stats, 1, 1, 0, s));
   return ADMM_OK;
@@ -1371,7 +1409,10 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   C->P_fwd = C->mm ? (int)((C->half->mrays + kBlock - 1) / kBlock)
            : (C->n_groups > 0 || C->csr) ? (int)((m + kBlock - 1) / kBlock)
                                          : ((C->g.n_det + kFwdRays - 1) / kFwdRays) * C->g.n_angles;
-  C->P_edge = B.z ? (int)((npix + kBlock * 4 - 1) / (kBlock * 4)) : (int)((npix + kConsPix - 1) / kConsPix);
+  // partials per (edge, 64-pixel block) for the midpoint kernels (stored or derived z), per
+  // (edge, 1024 pixels) for the weighted one
+  C->P_edge = B.fusion == ADMM_FUSE_WEIGHTED ? (int)((npix + kBlock * 4 - 1) / (kBlock * 4))
+                                             : (int)((npix + kConsPix - 1) / kConsPix);
   RET(ensure(C->partH, (size_t)5 * V * C->P_back * 8));
   RET(ensure(C->partS, (size_t)V * C->P_fwd * 8));
   RET(ensure(C->partD, (size_t)5 * V * C->P_back * 8));
@@ -1483,41 +1524,50 @@ int admm_consensus(admm_ctx* C, void* stream) {
 }
 
 extern "C++" {
+// One x-update enqueued directly (the graph's launch sequence, no graph) with timing-only
+// events around every in-solve launch of `kind` (0: the forward tap kernel of each CG step,
+// right after the CG / TV update that wrote p and p^T; 1: the back projector of each CG step,
+// right after its forward combine), exactly as in every replay; ms = their average duration.
 template <typename T>
-int time_fwd(admm_ctx* C, int reps, int in_solve, hipStream_t s, float* ms) {
+int time_in_solve(admm_ctx* C, int kind, hipStream_t s, float* ms) {
   return with_vb(C->vb, [&](auto vbc) -> int {
     constexpr int VB = decltype(vbc)::value;
-    if (in_solve) {
-      // one x-update enqueued directly (the graph's launch sequence, no graph), with events
-      // around each CG step's forward tap launch: the predecessor is the CG / TV update that
-      // just wrote p and p^T, exactly as in every replay
-      const int n = C->b.tv_iters * C->b.cg_iters;
-      std::vector<hipEvent_t> ev(2 * n);
-      // timing-only events: no system-scope fence (cache writeback / invalidation) at each
-      // record, which would perturb the launches they bracket
-      for (auto& e : ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
-      C->tf_ev = &ev;
-      C->tf_next = 0;
-      const bool keep = (C->b.flags & ADMM_BATCH_KEEP_X) != 0;
-      int rc = enqueue_update<T, VB>(C, s, keep && C->ats_valid);
-      const size_t used = C->tf_next;
-      C->tf_ev = nullptr;
-      if (rc == ADMM_OK && keep) C->ats_valid = true;
-      if (rc == ADMM_OK && used == 0) rc = fail(ADMM_E_STATE, "no forward launch was timed");
-      if (rc == ADMM_OK) {
-        HIPCHK(hipEventSynchronize(ev[used - 1]));
-        float tot = 0.f;
-        for (size_t i = 0; i < used; i += 2) {
-          float t = 0.f;
-          HIPCHK(hipEventElapsedTime(&t, ev[i], ev[i + 1]));
-          tot += t;
-        }
-        *ms = tot / (float)(used / 2);
+    const int n = C->b.tv_iters * C->b.cg_iters;
+    std::vector<hipEvent_t> ev(2 * n);
+    // no system-scope fence (cache writeback / invalidation) at each record, which would
+    // perturb the launches they bracket
+    for (auto& e : ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+    C->tf_ev = &ev;
+    C->tf_next = 0;
+    C->tf_kind = kind;
+    const bool keep = (C->b.flags & ADMM_BATCH_KEEP_X) != 0;
+    int rc = enqueue_update<T, VB>(C, s, keep && C->ats_valid);
+    const size_t used = C->tf_next;
+    C->tf_ev = nullptr;
+    C->tf_kind = 0;
+    if (rc == ADMM_OK && keep) C->ats_valid = true;
+    if (rc == ADMM_OK && used == 0) rc = fail(ADMM_E_STATE, "no launch was timed");
+    if (rc == ADMM_OK) {
+      HIPCHK(hipEventSynchronize(ev[used - 1]));
+      float tot = 0.f;
+      for (size_t i = 0; i < used; i += 2) {
+        float t = 0.f;
+        HIPCHK(hipEventElapsedTime(&t, ev[i], ev[i + 1]));
+        tot += t;
       }
-      for (auto& e : ev) (void)hipEventDestroy(e);
-      return rc;
+      *ms = tot / (float)(used / 2);
     }
-    // the dominant kernel alone, back to back: k_fwdg (every sample tap) when grouped, else k_fwd
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    return rc;
+  });
+}
+
+template <typename T>
+int time_fwd(admm_ctx* C, int reps, int in_solve, hipStream_t s, float* ms) {
+  if (in_solve) return time_in_solve<T>(C, 0, s, ms);
+  return with_vb(C->vb, [&](auto vbc) -> int {
+    constexpr int VB = decltype(vbc)::value;
+    // the forward tap kernel alone, back to back: k_fwdg (every sample tap) when grouped, else k_fwd
     auto one = [&]() -> int {
       if (C->n_groups > 0) return launch_fwdg_taps<T, VB>(C, (T*)C->xs.p, (T*)C->xsT.p, C->b.V, s);
       return launch_fwd<T, VB, 0>(C, (T*)C->xs.p, (T*)C->xsT.p, (T*)C->sino.p, nullptr, nullptr, C->b.V, s);
@@ -1548,6 +1598,28 @@ int admm_time_forward(admm_ctx* C, int reps, int in_solve, void* stream, double*
   RET(C->dtype == ADMM_DTYPE_F32 ? time_fwd<float>(C, reps, in_solve, s, &ms)
                                   : time_fwd<double>(C, reps, in_solve, s, &ms));
   *ms_out = in_solve ? (double)ms : (double)ms / reps;
+  return ADMM_OK;
+}
+
+int admm_consensus_range(admm_ctx* C, int e0, int e1, int rows, void* stream) {
+  if (!C || !C->bound) return fail(ADMM_E_STATE, "no batch bound");
+  const admm_batch& B = C->b;
+  if (B.z == nullptr || B.fusion != ADMM_FUSE_MIDPOINT)
+    return fail(ADMM_E_STATE, "admm_consensus_range needs stored z and midpoint fusion");
+  if (e0 < 0 || e1 < e0 || e1 > B.n_edges) return fail(ADMM_E_INVALID, "edge range out of bounds");
+  if (rows < 1 || rows > B.n_xext) return fail(ADMM_E_INVALID, "rows out of range");
+  DEVICE_SCOPE(C->device);
+  return enqueue_consensus_stored(C, e0, e1, rows, (hipStream_t)stream);
+}
+
+int admm_time_back(admm_ctx* C, void* stream, double* ms_out) {
+  if (!C || !C->bound) return fail(ADMM_E_STATE, "no batch bound");
+  if (!ms_out) return fail(ADMM_E_INVALID, "bad argument");
+  DEVICE_SCOPE(C->device);
+  hipStream_t s = (hipStream_t)stream;
+  float ms = 0.f;
+  RET(C->dtype == ADMM_DTYPE_F32 ? time_in_solve<float>(C, 1, s, &ms) : time_in_solve<double>(C, 1, s, &ms));
+  *ms_out = (double)ms;
   return ADMM_OK;
 }
 

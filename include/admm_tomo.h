@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ADMM_ABI_VERSION 8
+#define ADMM_ABI_VERSION 9
 
 #define ADMM_OK 0
 #define ADMM_E_INVALID (-1)
@@ -231,6 +231,20 @@ int admm_fwd_plan_info(admm_ctx* ctx, int plan, int* groups, int* blocks, double
  * full-width sample vectors even for narrow batches; admm_fwd_plan_info then reports the half
  * geometry's plans).  No device work. */
 int admm_batch_info(admm_ctx* ctx, int* vb, int* mirror);
+/* ABI 9: admm_consensus for the edge slots [e0, e1) only (stored z, midpoint fusion), whose
+ * endpoints must all lie in x_ext rows [0, rows) -- the caller's promise; only those rows are
+ * read.  With the rank-internal edges (both endpoints local, rows < V) first in slot order
+ * (admm_hip/plan.py), a rank runs them while the halo exchange is still writing rows >= V, then
+ * the rest: the same per-edge arithmetic and statistics as one admm_consensus, bitwise.
+ * Replaces block_6_admm_loop_ver2.py:210-253 for those edges.  Enqueued directly (no graph). */
+int admm_consensus_range(admm_ctx* ctx, int e0, int e1, int rows, void* stream);
+/* ABI 9: average duration (ms) of the bound batch's back projector launch inside the CG solve
+ * (the adjoint `Ai.T @ r` of block_6_admm_loop_ver2.py:145 fused with the CG operator
+ * H p = A^T A p + rho D p + mu K^T K p and its dot products): one x-update is enqueued directly
+ * with HIP events around each CG step's back projection (right after its forward combine, as in
+ * every solve); the batch's state advances by that x-update.  Measurement helper for bench.py's
+ * roofline of the dominant kernel; synchronises. */
+int admm_time_back(admm_ctx* ctx, void* stream, double* ms_out);
 
 /* --- per-pixel edge masks for masked precisions (setup) --- */
 

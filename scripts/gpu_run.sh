@@ -38,7 +38,8 @@ for step in "$@"; do
     tests=*)
       expr=${step#tests=}
       if [ "$expr" = all ]; then k=(); else k=(-k "$expr"); fi
-      run pytest 1100 python -u -m pytest tests -m gpu "${k[@]}" -q -rf --timeout 600 --timeout-method thread --durations=15 > gpurun_out/pytest_${TAG}.log 2>&1
+      # -s: tests that run minutes (the 20-iteration C3 oracle) print progress lines to the log
+      run pytest 1100 python -u -m pytest tests -m gpu "${k[@]}" -v -s -rf --timeout 900 --timeout-method thread --durations=15 > gpurun_out/pytest_${TAG}.log 2>&1
       rc=$?; tail -25 gpurun_out/pytest_${TAG}.log; [ $rc -ne 0 ] && exit $rc ;;
     prof|profm|profd)  # prof: default modes; profm / profd: mirror-mode forward forced on / off
       mm=; [ $step = profm ] && mm=1; [ $step = profd ] && mm=0
@@ -68,9 +69,9 @@ for step in "$@"; do
     benchallm)  # benchall with the mirror-mode forward
       ADMM_FWD_MIRROR=1 run benchallm 900 python bench.py --steps 20 --warmup 5 --proxy all --no-cpu-baseline > gpurun_out/benchallm_${TAG}.json 2> gpurun_out/benchallm_${TAG}.err || { tail -5 gpurun_out/benchallm_${TAG}.err; exit 1; }
       python scripts/summarize_bench.py gpurun_out/benchallm_${TAG}.json ;;
-    share=*)  # share=CONFIG:R/W[:z]: one rank's share on this GPU (bench --as-rank; z: --stored-z A/B)
+    share=*)  # share=CONFIG:R/W[:d]: one rank's share on this GPU (bench --as-rank; d: --edge-state derived A/B)
       v=${step#share=}; cfg=${v%%:*}; rest=${v#*:}; rw=${rest%%:*}; sz=()
-      case $rest in *:z) sz=(--stored-z) ;; esac
+      case $rest in *:d) sz=(--edge-state derived) ;; esac
       out=gpurun_out/share_${cfg}_${rw/\//of}${sz:+_z}_${TAG}.json
       run $step 600 python bench.py --config $cfg --as-rank $rw --steps 4 --warmup 2 "${sz[@]}" > $out 2> ${out%.json}.err || { tail -5 ${out%.json}.err; exit 1; }
       tail -c 600 $out ;;

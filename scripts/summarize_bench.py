@@ -3,10 +3,12 @@ import json
 import sys
 
 b = json.loads([l for l in open(sys.argv[1]) if l.strip().startswith("{")][-1])
-r = b["roofline"]
+r = b.get("roofline_fwd", b["roofline"])
+rb = b.get("roofline_back")
 print(f"headline {b['value']:.1f} {b['unit']} ({b['ms_per_step']:.3f} ms/step, {b['config']['nodes']} nodes, "
       f"{b['n_gpus']} GPU)  fwd {r['avg_launch_ms'] * 1e3:.2f} us (b2b {r['avg_launch_ms_back_to_back'] * 1e3:.2f}) "
-      f"frac {r['frac']}  lds {r['lds']['frac']:.3f}")
+      f"frac {r['frac']}  lds {r['lds']['frac']:.3f}"
+      + (f"  back {rb['avg_launch_ms'] * 1e3:.2f} us frac {rb['frac']} lds {rb['lds']['frac']:.3f}" if rb else ""))
 if "cpu_baseline" in b:
     c = b["cpu_baseline"]
     print(f"cpu {c['value']:.2f} {c['unit']} on {c['cores']} cores, rel_fro {c['rel_fro']:.2e}")
@@ -19,7 +21,9 @@ for k, p in sorted(b.get("proxy_8gpu", {}).items()):
         continue
     sh = " | ".join(f"r{s['rank']}: V={s['local_nodes']} vb={s['vb']} H={s['halo_rows']} E={s['stored_edges']} "
                     f"{s['ms_per_step']:.2f} ms (cons {s.get('consensus_ms', float('nan')):.2f}) + ex "
-                    f"{s['exchange']['ms_direct']:.2f} ({s['exchange']['mode']})"
+                    f"{s['exchange'].get('ms_conservative', s['exchange']['ms_direct']):.2f} ({s['exchange']['mode']}) "
+                    f"z {s.get('z', '?')}"
                     for s in p["shares"])
     print(f"proxy {k}: T1 {p['T1_ms_per_step']:.2f} ms, per-node ratio {p['per_node_cost_ratio']:.3f}, "
-          f"speedup {p['predicted_speedup']:.2f}x (one link {p['predicted_speedup_one_link']:.2f}x)  [{sh}]")
+          f"speedup {p['predicted_speedup']:.2f}x (one link {p['predicted_speedup_one_link']:.2f}x, direct "
+          f"{p.get('predicted_speedup_direct', float('nan')):.2f}x)  [{sh}]")

@@ -69,3 +69,21 @@ def test_c4_graph_matches_committed_adjacency():
     assert G.number_of_nodes() == fx["nodes"] == 32 and nx.is_connected(G)
     assert sorted([list(e) for e in G.edges()]) == fx["edges"]
     assert len(fx["edges"]) == 103
+
+
+def test_roofline_traffic_lookup_finds_committed_kernels():
+    """bench.py's roofline reads both projectors' PMC bytes per launch from the committed
+    traffic files by their full template names (mirror mode at C3: 4-node real vectors,
+    8-lane virtual ones)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    tr, f = bench.pmc_traffic("C3")
+    assert tr is not None, f
+    back = bench.back_kernel_traffic(tr, "float", 4, True)
+    fwd = bench.fwd_kernel_traffic(tr, "float", 4, True)
+    assert back is not None and fwd is not None
+    # compulsory bytes of the C3 back launch (16 nodes, 512^2, 96 angles): sinogram + p + D + Hp
+    # as float32 samples and r as float64 -- the PMC traffic exceeds it
+    V, n, m = 16, 512 * 512, 96 * 512
+    assert back > V * m * 4 + 3 * V * n * 4 + V * n * 8
+    assert fwd > V * n * 4 + V * m * 4

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
         assert name in _lib.SYMBOLS, f"{name} not bound in _lib.SYMBOLS"
     assert set(_lib.SYMBOLS) == set(names)
-    assert lib.admm_abi_version() == _lib.ABI_VERSION == 8
+    assert lib.admm_abi_version() == _lib.ABI_VERSION == 9
 
 
 def test_error_path_without_gpu_work():

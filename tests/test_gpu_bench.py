@@ -40,8 +40,14 @@ def test_bench_line_contract(cuda):
     assert r["bound"] in ("hbm", "mfma") and 0 < r["frac"] <= 1
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
     assert 0 < r["lds"]["frac"] <= 1
+    # the dominant kernel is the projector with the longer in-solve launch; both are reported
+    rf, rb = b["roofline_fwd"], b["roofline_back"]
+    assert r["kernel"] == max((rf, rb), key=lambda x: x["avg_launch_ms"])["kernel"]
+    assert rb["kernel"].startswith("k_back") and rf["kernel"].startswith("k_fwdg")
+    for x in (rf, rb):
+        assert 0 < x["frac"] <= 1 and 0 < x["lds"]["frac"] <= 1 and x["traffic"] > x["compulsory_bytes"]
     # the bound forward plan at 512^2 runs in one round (<= 2 blocks per CU)
-    assert r["fwd_plan"]["active"] and r["fwd_plan"]["blocks"] <= 512, r["fwd_plan"]
+    assert rf["fwd_plan"]["active"] and rf["fwd_plan"]["blocks"] <= 512, rf["fwd_plan"]
     assert "workload" in b["config"] and "model" not in b["config"]
 
 

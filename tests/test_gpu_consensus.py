@@ -109,9 +109,10 @@ def _ring_run(V, world=1, rank=0, port=None, q=None):
 
 
 @pytest.mark.timeout(300)
-def test_lds_and_direct_consensus_kernels_agree_bitwise(cuda):
+def test_lds_and_direct_consensus_kernels_agree_bitwise(cuda, monkeypatch):
     import torch.multiprocessing as mp
     V = 130  # one rank: 130 x_ext rows (> 128: direct kernel); two ranks: 65 + 2 (LDS tile)
+    monkeypatch.setenv("ADMM_EDGE_STATE", "derived")  # (stored z is the default wherever it fits)
     x1, p1, d1 = _ring_run(V)
     port = _free_port()
     ctx = mp.get_context("spawn")

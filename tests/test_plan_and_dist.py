@@ -115,7 +115,7 @@ def _free_port():
     return p
 
 
-def _sharded_oracle_admm(rank, world, port, gname, out_q):
+def _sharded_oracle_admm(rank, world, port, gname, out_q, overlap=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (os.path.join(os.path.dirname(here), "distributed-inverse-problem-admm_amd"),
@@ -127,7 +127,7 @@ def _sharded_oracle_admm(rank, world, port, gname, out_q):
     try:
         from admm_hip.exchange import HaloExchange, assemble_stats, gather_images
         from admm_hip.plan import make_plan
-        res = run_sharded(rank, world, gname, HaloExchange, assemble_stats, gather_images, make_plan)
+        res = run_sharded(rank, world, gname, HaloExchange, assemble_stats, gather_images, make_plan, overlap)
         out_q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -173,8 +173,11 @@ def test_subset_plans_of_operator_groups():
     assert sorted(owned) == sorted(ge for k, ge in enumerate(rp.stored_edges) if rp.owned_edge[k])
 
 
-def run_sharded(rank, world, gname, HaloExchange, assemble_stats, gather_images, make_plan):
-    """The device loop of admm_hip.admm.run_admm with the oracle in place of the kernels."""
+def run_sharded(rank, world, gname, HaloExchange, assemble_stats, gather_images, make_plan, overlap=False):
+    """The device loop of admm_hip.admm.run_admm with the oracle in place of the kernels.
+    ``overlap``: RankGroups.exchange_consensus's order -- the exchange issued asynchronously
+    (HaloExchange.start), the internal edge slots [0, n_internal) updated from the local rows
+    while it is in flight, then the halo rows landed (finish) and the remaining slots updated."""
     from oracle import node_solver as ons
     G, V, N, A, ph, sinos, W = problem(gname)
     n = N * N
@@ -203,18 +206,29 @@ def run_sharded(rank, world, gname, HaloExchange, assemble_stats, gather_images,
             d = ons.node_update(A, A.T @ sinos[g], sinos[g], D, c, qv, states[g], N, prm)
             x_ext[r] = torch.from_numpy(states[g].x)
             node_stats[r] = torch.tensor([d.mse_sino, d.g_norm ** 2, d.tv, d.quad, 0.0, d.sb_res ** 2])
-        halo.run()
-        xs = x_ext.numpy()
         edge_stats = torch.zeros((max(E, 1), 3), dtype=torch.float64)
-        for s, (ra, rb) in enumerate(zip(plan.edge_a_row, plan.edge_b_row)):
-            xa, xb = xs[ra], xs[rb]
-            aa, ab = xa + y[s], xb - y[s]
-            zn = (aa + ab) * 0.5
-            y[s] = y[s] + xa - zn
-            dz = zn - z[s]
-            z[s] = zn
-            edge_stats[s] = torch.tensor([float((xa - zn) @ (xa - zn)), float((xb - zn) @ (xb - zn)),
-                                          float(dz @ dz)])
+
+        def edges(s0, s1, rows):
+            xs = x_ext[:rows].numpy()
+            for s in range(s0, s1):
+                ra, rb = plan.edge_a_row[s], plan.edge_b_row[s]
+                assert ra < rows and rb < rows
+                xa, xb = xs[ra], xs[rb]
+                aa, ab = xa + y[s], xb - y[s]
+                zn = (aa + ab) * 0.5
+                y[s] = y[s] + xa - zn
+                dz = zn - z[s]
+                z[s] = zn
+                edge_stats[s] = torch.tensor([float((xa - zn) @ (xa - zn)), float((xb - zn) @ (xb - zn)),
+                                              float(dz @ dz)])
+        if overlap:
+            h = halo.start()
+            edges(0, plan.n_internal, plan.V)  # both endpoints local: rows < V
+            halo.finish(h)
+            edges(plan.n_internal, E, plan.n_xext)
+        else:
+            halo.run()
+            edges(0, E, plan.n_xext)
         ns, es = assemble_stats(plan, node_stats, edge_stats[:E])
         r2 = sum(float(es[ge, 0]) + float(es[ge, 1]) for ge in range(len(plan.edges)))
         s2 = sum(rho * rho * float(es[ge, 2]) for ge in range(len(plan.edges)))
@@ -256,6 +270,36 @@ def test_gloo_sharded_matches_single_process_bitwise(gname, world):
     assert np.abs(np.stack(xo) - X1).max() <= 1e-10 * np.abs(X1).max()
     assert np.allclose(ho["primal"], h1["primal"], rtol=1e-7, atol=0)
     assert np.allclose(ho["dual"], h1["dual"], rtol=1e-7, atol=0)
+
+
+@pytest.mark.parametrize("gname,world", [("er9", 4), ("ring8", 4), ("complete6", 2)])
+def test_gloo_overlapped_exchange_matches_serial_bitwise(gname, world):
+    """RankGroups.exchange_consensus's order (rank-internal edges updated while the halo images
+    are in flight: asynchronous all-gather on ER / complete graphs, p2p on the ring) gives the
+    serial exchange-then-consensus run bitwise, and the single-process run."""
+    from admm_hip.exchange import HaloExchange, assemble_stats, gather_images
+    X1, h1 = run_sharded(0, 1, gname, HaloExchange, assemble_stats, gather_images, make_plan)
+    # internal edges (some rank has them to overlap) come first in slot order
+    G = dict(graphs())[gname]
+    assert any(make_plan(G, G.number_of_nodes(), world, r).n_internal for r in range(world))
+    for r in range(world):
+        p = make_plan(G, G.number_of_nodes(), world, r)
+        assert all(p.edge_a_row[k] < p.V and p.edge_b_row[k] < p.V for k in range(p.n_internal))
+        assert all(max(p.edge_a_row[k], p.edge_b_row[k]) >= p.V for k in range(p.n_internal, len(p.stored_edges)))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_oracle_admm, args=(r, world, port, gname, q, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        X2, h2 = res[r]
+        assert np.array_equal(X1, X2), gname
+        assert h1["primal"] == h2["primal"] and h1["dual"] == h2["dual"], gname
 
 
 def _placement_rank(rank, world, port, q):
@@ -350,3 +394,96 @@ def test_verify_halo_detects_exchange_errors(gname, world):
         assert before == {"halo_rows": total, "mismatched_rows": total}
         assert after == {"halo_rows": total, "mismatched_rows": 0}
         assert flipped == {"halo_rows": total, "mismatched_rows": flips}
+
+
+# ---------------------------------------------------------------------------------------
+# the run's one edge-state rule (stored vs derived z; plan.z_is_stored, groups.py)
+# ---------------------------------------------------------------------------------------
+class _Op:
+    """Host stand-in of a RayTransform for the batch-grouping logic (operator_key)."""
+
+    def __init__(self, N, a, dtype="float32"):
+        from admm_hip.geometry import ParallelBeamGeometry
+        self.geom = ParallelBeamGeometry(N, a)
+        self.dtype = dtype
+        self.device = 0
+
+
+HBM_MI355X = 288 * 10**9
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_stored_z_for_every_baseline_config_at_every_gpu_count(world):
+    """C3 (16-node ring, 512^2), C4 (32-node ER, 1024^2), C5 (64-node complete,
+    2048^2, float64): the stored edge state (y, z) of the busiest rank fits the rule's share of 288 GB
+    at 1, 2, 4 and 8 GPUs -- stored z (faster, profiles/r4_shares_derived_vs_stored_z.txt)
+    everywhere, so one problem runs the same edge arithmetic at every GPU count (the 1-rank
+    vs N-rank bitwise tests need that)."""
+    from admm_hip.groups import stored_edges_per_rank
+    from admm_hip.plan import z_is_stored
+    sg = dict(scale_graphs())
+    cases = [("C3", nx.cycle_graph(16), 16, 512, "float32"), ("C4", sg["er32"], 32, 1024, "float32"),
+             ("C5", sg["complete64"], 64, 2048, "float64")]
+    for name, G, V, N, dt in cases:
+        ops = [_Op(N, 96, dt)] * V
+        per = stored_edges_per_rank(ops, G, V, world)
+        assert len(per) == world
+        assert z_is_stored(per, N * N, HBM_MI355X), (name, world, per)
+    # C5 on one GPU is two batches (56 + 8 nodes: 32-bit offsets), the cross edges stored twice
+    assert stored_edges_per_rank([_Op(2048, 96, "float64")] * 64, sg["complete64"], 64, 1) == [2464]
+
+
+def test_derived_z_when_stored_would_not_fit():
+    """A graph whose stored edge state exceeds the rule's share of HBM derives z (weighted
+    fusion never)."""
+    from admm_hip.groups import stored_edges_per_rank
+    from admm_hip.plan import STORED_Z_HBM_FRACTION, stored_edge_state_bytes, z_is_stored
+    G = nx.complete_graph(48)
+    per = stored_edges_per_rank([_Op(2048, 96, "float64")] * 48, G, 48, 1)
+    assert per == [48 * 47 // 2]
+    hbm = int(stored_edge_state_bytes(per, 2048 * 2048) / STORED_Z_HBM_FRACTION) - 1
+    assert not z_is_stored(per, 2048 * 2048, hbm)
+    assert z_is_stored(per, 2048 * 2048, hbm + 1)
+    assert z_is_stored(per, 2048 * 2048, hbm, fusion="weighted")
+
+
+def _z_rule_rank(rank, world, port, hbm, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from admm_hip.groups import min_over_ranks, stored_edges_per_rank
+        from admm_hip.plan import z_is_stored
+        # every rank weighs the same global inputs; the device HBM is agreed by one MIN all-reduce
+        # (rank 1 here reports a smaller device, so the agreed HBM derives z on every rank)
+        G = nx.complete_graph(48)
+        per = stored_edges_per_rank([_Op(2048, 96, "float64")] * 48, G, 48, world)
+        agreed = min_over_ranks(hbm[rank], world)
+        q.put((rank, agreed, z_is_stored(per, 2048 * 2048, agreed)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_z_rule_same_answer_on_every_rank(world):
+    """The rule is one global decision: with per-rank device HBM that differs (rank 1 smaller,
+    below the C5-like graph's threshold), every rank of a gloo world 2 / 4 / 8 gets the same
+    HBM from the MIN all-reduce and the same stored / derived answer."""
+    from admm_hip.groups import stored_edges_per_rank
+    from admm_hip.plan import STORED_Z_HBM_FRACTION, stored_edge_state_bytes
+    per = stored_edges_per_rank([_Op(2048, 96, "float64")] * 48, nx.complete_graph(48), 48, world)
+    need = int(stored_edge_state_bytes(per, 2048 * 2048) / STORED_Z_HBM_FRACTION)
+    hbm = [need + 10**9] * world
+    hbm[1] = need - 10**9
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_z_rule_rank, args=(r, world, port, hbm, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert {r[1] for r in res} == {need - 10**9}
+    assert {r[2] for r in res} == {False}
