@@ -268,10 +268,13 @@ int build_fwd_order(admm_ctx* C, int pl, int nch, int cus) {
 // single round, where the 64-ray plan's equal segment shares keep every XCD on its own row
 // band (512^2, one chunk: 33 us against 35-37 for the clipped plans).
 // ADMM_FWD_PLAN=0..5 forces a plan.
-template <typename T, int VB>
+// MIRROR / VBR: the instantiation launch_fwdg_taps launches (mirror mode: k_fwdg<T, VBV, true,
+// VBR>, whose piece state and second window buffer set its own registers and LDS), so the
+// occupancy query prices the kernel that actually runs.
+template <typename T, int VB, bool MIRROR = false, int VBR = VB>
 int pick_fwd_plan(admm_ctx* C, int nch, int* pl_out, int* cus_out) {
   int per_cu = 0, cus = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fwdg<T, VB>, kFgThreads, 0));
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fwdg<T, VB, MIRROR, VBR>, kFgThreads, 0));
   HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, C->device));
   if (per_cu < 1) return fail(ADMM_E_HIP, "grouped forward projector cannot be resident");
   const long slots = (long)per_cu * std::max(1, cus);
@@ -289,12 +292,12 @@ int pick_fwd_plan(admm_ctx* C, int nch, int* pl_out, int* cus_out) {
   return ADMM_OK;
 }
 
-template <typename T, int VB>
+template <typename T, int VB, bool MIRROR = false, int VBR = VB>
 int choose_fwd_plan(admm_ctx* C, int V) {
   if (C->plan_n[0] == 0) return ADMM_OK;
   const int nch = (V + VB - 1) / VB;
   int pl = 0, cus = 0;
-  RET((pick_fwd_plan<T, VB>(C, nch, &pl, &cus)));
+  RET((pick_fwd_plan<T, VB, MIRROR, VBR>(C, nch, &pl, &cus)));
   select_fwd_plan(C, pl);
   return getenv("ADMM_FWD_NATURAL_ORDER") && getenv("ADMM_FWD_NATURAL_ORDER")[0] == '1'
              ? build_fwd_order(C, pl, nch, 0)
@@ -364,10 +367,10 @@ int bind_fwd_plan(admm_ctx* C, int V) {
                                                                                       : mirror_vb<double, VBR>()));
       if (C->dtype == ADMM_DTYPE_F32) {
         constexpr int VBV = mirror_vb<float, VBR>();
-        return choose_fwd_plan<float, VBV>(C->half, nchv * VBV);
+        return choose_fwd_plan<float, VBV, true, VBR>(C->half, nchv * VBV);
       }
       constexpr int VBV = mirror_vb<double, VBR>();
-      return choose_fwd_plan<double, VBV>(C->half, nchv * VBV);
+      return choose_fwd_plan<double, VBV, true, VBR>(C->half, nchv * VBV);
     }));
   } else {
     RET(with_vb(C->vb, [&](auto vbc) {

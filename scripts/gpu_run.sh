@@ -41,6 +41,15 @@ for step in "$@"; do
       # -s: tests that run minutes (the 20-iteration C3 oracle) print progress lines to the log
       run pytest 1100 python -u -m pytest tests -m gpu "${k[@]}" -v -s -rf --timeout 900 --timeout-method thread --durations=15 > gpurun_out/pytest_${TAG}.log 2>&1
       rc=$?; tail -25 gpurun_out/pytest_${TAG}.log; [ $rc -ne 0 ] && exit $rc ;;
+    etests=*)  # etests=VAR=VAL:EXPR -- pytest -m gpu -k EXPR with VAR=VAL in the environment (A/B of a kernel switch)
+      v=${step#etests=}; kv=${v%%:*}; expr=${v#*:}
+      env "$kv" timeout -k 10 1100 python -u -m pytest tests -m gpu -k "$expr" -v -s -rf --timeout 900 --timeout-method thread > gpurun_out/etests_${TAG}.log 2>&1
+      rc=$?; tail -15 gpurun_out/etests_${TAG}.log; [ $rc -ne 0 ] && exit $rc ;;
+    envhl=*)  # envhl=VAR=VAL[@WORKLOAD]: headline only (no CPU baseline) with VAR=VAL in the environment
+      v=${step#envhl=}; wl=C3; case $v in *@*) wl=${v#*@}; v=${v%@*} ;; esac
+      nm=$(echo "$v" | tr '=' '_')
+      env "$v" timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --headline-only --workload $wl > gpurun_out/envhl_${nm}_${wl}_${TAG}.json 2> gpurun_out/envhl_${nm}_${wl}_${TAG}.err || { tail -5 gpurun_out/envhl_${nm}_${wl}_${TAG}.err; exit 1; }
+      python scripts/summarize_bench.py gpurun_out/envhl_${nm}_${wl}_${TAG}.json ;;
     prof|profm|profd)  # prof: default modes; profm / profd: mirror-mode forward forced on / off
       mm=; [ $step = profm ] && mm=1; [ $step = profd ] && mm=0
       ADMM_FWD_MIRROR=$mm run $step 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${step}_${TAG} -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --headline-only > gpurun_out/${step}_${TAG}.log 2>&1 || exit 1

@@ -41,14 +41,17 @@ def _run(N, V, a_per, dtype, iters=3, graph="ring"):
     return ops, ph, sinos, Q, G, np.stack(x), h
 
 
-@pytest.mark.parametrize("dtype,V,mode", [("float32", 1, "1"), ("float32", 2, "1"), ("float32", 4, "1"),
-                                          ("float32", 8, "1"), ("float32", 12, "1"), ("float64", 1, "1"),
-                                          ("float64", 2, "1"), ("float64", 4, "1"),
-                                          ("float32", 4, "0"), ("float32", 12, "0")])
-def test_mirror_trajectory_matches_oracle(cuda, monkeypatch, dtype, V, mode):
-    """mode "1": mirror mode at every node-interleave width; "0": the direct projection."""
+@pytest.mark.parametrize("dtype,V,mode,N", [("float32", 1, "1", 48), ("float32", 2, "1", 48), ("float32", 4, "1", 48),
+                                            ("float32", 8, "1", 48), ("float32", 12, "1", 48), ("float64", 1, "1", 48),
+                                            ("float64", 2, "1", 48), ("float64", 4, "1", 48),
+                                            ("float32", 4, "0", 48), ("float32", 12, "0", 48),
+                                            ("float32", 1, "1", 47), ("float32", 4, "1", 47), ("float32", 8, "1", 47),
+                                            ("float64", 2, "1", 47)])
+def test_mirror_trajectory_matches_oracle(cuda, monkeypatch, dtype, V, mode, N):
+    """mode "1": mirror mode at every node-interleave width; "0": the direct projection.  Odd
+    N (47): the middle row pairs with itself in the back projectors' pixel pairs."""
     monkeypatch.setenv("ADMM_FWD_MIRROR", mode)
-    N, a = 48, 24
+    a = 24
     ops, ph, sinos, Q, G, x, h = _run(N, V, a, dtype)
     A = joseph_matrix(Geometry(N, a))
     xo, ho = oadmm.decentralized_admm([A] * V, [s.double().cpu().numpy() for s in sinos], G, Q, N, lam_tv=0.02,
@@ -63,16 +66,17 @@ def test_mirror_trajectory_matches_oracle(cuda, monkeypatch, dtype, V, mode):
     assert all(v < tol for v in errs.values()), errs
 
 
-@pytest.mark.parametrize("dtype,mode", [("float32", "1"), ("float64", "1"), ("float32", "0")])
-def test_mirror_result_independent_of_batch_size(cuda, monkeypatch, dtype, mode):
+@pytest.mark.parametrize("dtype,mode,N", [("float32", "1", 40), ("float64", "1", 40), ("float32", "0", 40),
+                                         ("float32", "1", 47)])
+def test_mirror_result_independent_of_batch_size(cuda, monkeypatch, dtype, mode, N):
     """Node 0 of an edgeless graph (its x-update sees only its own data) in batches of 1, 2,
     3, 4, 8 nodes -- every node-interleave width and both staging paths (LDS-DMA and the
     register path of the narrow widths) -- bitwise the same image and statistics (mirror
-    mode, and the direct projection)."""
+    mode, and the direct projection; odd N: the self-paired middle row)."""
     monkeypatch.setenv("ADMM_FWD_MIRROR", mode)
     res = {}
     for V in (1, 2, 3, 4, 8):
-        _, _, _, _, _, x, h = _run(40, V, 16, dtype, iters=2, graph="empty")
+        _, _, _, _, _, x, h = _run(N, V, 16, dtype, iters=2, graph="empty")
         res[V] = (x[0], np.stack(h["mse_sino_per_node"])[:, 0], np.stack(h["obj_per_node"])[:, 0])
     for V, r in res.items():
         assert np.array_equal(r[0], res[1][0]), V
