@@ -734,35 +734,21 @@ int enqueue_update_any(admm_ctx* C, hipStream_t s, bool reuse = false, int round
 // rows of the derived consensus' LDS tile (0: more x_ext rows than any tile: direct kernel)
 int cons_rows(int n_xext) { return n_xext <= 16 ? 16 : n_xext <= 64 ? 64 : n_xext <= 128 ? 128 : 0; }
 
-// stored-z midpoint consensus of edge slots [e0, e1) whose endpoints lie in x_ext rows [0, R)
-// (k_consensus_stored; the LDS tile when R fits one, the same results otherwise)
-int enqueue_consensus_stored(admm_ctx* C, int e0, int e1, int R, hipStream_t s) {
+// stored-z midpoint consensus of edge slots [e0, e1) (k_consensus<false>: one edge per
+// blockIdx.y, 1024 pixels per block; the endpoint rows are read from HBM / L2 per edge -- at C5's
+// share, 476 edges over 64 rows, this streamed 48 B per pixel-edge in 14.1 ms against 17.4 ms for
+// a pixel-major LDS-tile variant, profiles/AB_LOG.md round 5)
+int enqueue_consensus_stored(admm_ctx* C, int e0, int e1, hipStream_t s) {
   const admm_batch& B = C->b;
   if (e1 <= e0) return ADMM_OK;
   const int npix = C->npix;
-  const dim3 g((npix + kConsPix - 1) / kConsPix);
-  double* part = (double*)C->partE.p;
-  switch (cons_rows(R)) {
-    case 16:
-      hipLaunchKernelGGL(k_consensus_stored<16>, g, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.edge_a, B.edge_b, part,
-                         npix, R, e0, e1);
-      break;
-    case 64:
-      hipLaunchKernelGGL(k_consensus_stored<64>, g, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.edge_a, B.edge_b, part,
-                         npix, R, e0, e1);
-      break;
-    case 128:
-      hipLaunchKernelGGL(k_consensus_stored<128>, g, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.edge_a, B.edge_b, part,
-                         npix, R, e0, e1);
-      break;
-    default:
-      hipLaunchKernelGGL(k_consensus_stored<0>, g, dim3(kBlock), 0, s, B.x_ext, B.y, B.z, B.edge_a, B.edge_b, part,
-                         npix, R, e0, e1);
-  }
+  dim3 grid((npix + kBlock * 4 - 1) / (kBlock * 4), e1 - e0);
+  hipLaunchKernelGGL(k_consensus<false>, grid, dim3(kBlock), 0, s, B.x_ext, B.y, nullptr, B.z, nullptr, B.edge_a,
+                     B.edge_b, (double*)C->partE.p, npix, e0);
   CHECK_LAUNCH();
   // rows 3 e0 .. 3 e1 - 1 of the partials -> edge_stats rows e0 .. e1 - 1
-  RET(launch_reduce(part + (size_t)3 * e0 * C->P_edge, 3 * (e1 - e0), C->P_edge, B.edge_stats + (size_t)3 * e0, 1, 1,
-                    0, s));
+  RET(launch_reduce((double*)C->partE.p + (size_t)3 * e0 * C->P_edge, 3 * (e1 - e0), C->P_edge,
+                    B.edge_stats + (size_t)3 * e0, 1, 1, 0, s));
   return ADMM_OK;
 }
 
@@ -799,7 +785,7 @@ int enqueue_consensus(admm_ctx* C, hipStream_t s) {
     RET(launch_reduce(part, 3 * B.n_edges, C->P_edge, B.edge_stats, 1, 1, 0, s));
     return ADMM_OK;
   }
-  if (B.fusion == ADMM_FUSE_MIDPOINT) return enqueue_consensus_stored(C, 0, B.n_edges, B.n_xext, s);
+  if (B.fusion == ADMM_FUSE_MIDPOINT) return enqueue_consensus_stored(C, 0, B.n_edges, s);
   dim3 grid((npix + kBlock * 4 - 1) / (kBlock * 4), B.n_edges);
   hipLaunchKernelGGL(k_consensus<true>, grid, dim3(kBlock), 0, s, B.x_ext, B.y, B.y_b, B.z, B.w, B.edge_a,
                      B.edge_b, (double*)C->partE.p, npix);
@@ -1412,10 +1398,9 @@ int admm_batch_bind(admm_ctx* C, const admm_batch* batch) {
   C->P_fwd = C->mm ? (int)((C->half->mrays + kBlock - 1) / kBlock)
            : (C->n_groups > 0 || C->csr) ? (int)((m + kBlock - 1) / kBlock)
                                          : ((C->g.n_det + kFwdRays - 1) / kFwdRays) * C->g.n_angles;
-  // partials per (edge, 64-pixel block) for the midpoint kernels (stored or derived z), per
-  // (edge, 1024 pixels) for the weighted one
-  C->P_edge = B.fusion == ADMM_FUSE_WEIGHTED ? (int)((npix + kBlock * 4 - 1) / (kBlock * 4))
-                                             : (int)((npix + kConsPix - 1) / kConsPix);
+  // partials per (edge, 1024 pixels) for the stored-z kernels, per (edge, 64-pixel block) for the
+  // derived-z ones
+  C->P_edge = B.z ? (int)((npix + kBlock * 4 - 1) / (kBlock * 4)) : (int)((npix + kConsPix - 1) / kConsPix);
   RET(ensure(C->partH, (size_t)5 * V * C->P_back * 8));
   RET(ensure(C->partS, (size_t)V * C->P_fwd * 8));
   RET(ensure(C->partD, (size_t)5 * V * C->P_back * 8));
@@ -1612,7 +1597,7 @@ int admm_consensus_range(admm_ctx* C, int e0, int e1, int rows, void* stream) {
   if (e0 < 0 || e1 < e0 || e1 > B.n_edges) return fail(ADMM_E_INVALID, "edge range out of bounds");
   if (rows < 1 || rows > B.n_xext) return fail(ADMM_E_INVALID, "rows out of range");
   DEVICE_SCOPE(C->device);
-  return enqueue_consensus_stored(C, e0, e1, rows, (hipStream_t)stream);
+  return enqueue_consensus_stored(C, e0, e1, (hipStream_t)stream);
 }
 
 int admm_time_back(admm_ctx* C, void* stream, double* ms_out) {

@@ -2410,9 +2410,9 @@ __global__ __launch_bounds__(kBlock) void k_consensus(const double* __restrict__
                                                       double* __restrict__ yb, double* __restrict__ z,
                                                       const double* __restrict__ w,
                                                       const int* __restrict__ ea, const int* __restrict__ eb,
-                                                      double* __restrict__ part, int npix) {
+                                                      double* __restrict__ part, int npix, int e0 = 0) {
   __shared__ double lds[12];
-  const int e = blockIdx.y;
+  const int e = e0 + blockIdx.y;  // (e0: admm_consensus_range's first slot)
   const size_t eo = (size_t)e * npix;
   const size_t ra_off = (size_t)ea[e] * npix, rb_off = (size_t)eb[e] * npix;
   const double* xa = xext + ra_off;
@@ -2557,74 +2557,6 @@ __global__ __launch_bounds__(kBlock) void k_consensus_derived_direct(const doubl
     if (lane == 0) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) part[((size_t)e * 3 + q) * P + blockIdx.x] = s[q];
-    }
-  }
-}
-
-// Stored-z midpoint consensus, pixel-major (the default edge state wherever it fits,
-// admm_hip/plan.py z_is_stored): k_consensus<false>'s arithmetic -- a_a = x_a + y, a_b = x_b - y,
-// z' = (a_a + a_b) * 0.5, y' = y + x_a - z' -- with k_consensus_derived's layout: a block owns 64
-// pixels (one per lane), stages the x_ext rows [0, R) of them in LDS once (RMAX > 0; RMAX = 0:
-// endpoint rows read from HBM / L2 per edge, the same results), and its 4 waves take every 4th
-// edge of [e0, e1): per edge y and z stream through HBM (32 B per pixel, against 48 B when both
-// endpoint rows are re-read per edge).  Partials per (edge, 64-pixel block), wave-reduced in a
-// fixed order -- the same for every RMAX, so a rank's result never depends on its row count.
-// The edge range lets the rank-internal edges (both endpoints local, rows < R = V) run while
-// the halo exchange is still writing the other rows (admm_consensus_range, ABI 9).
-template <int RMAX>
-__global__ __launch_bounds__(kBlock) void k_consensus_stored(const double* __restrict__ xext, double* __restrict__ y,
-                                                             double* __restrict__ z, const int* __restrict__ ea,
-                                                             const int* __restrict__ eb, double* __restrict__ part,
-                                                             int npix, int R, int e0, int e1) {
-  __shared__ double xn[RMAX > 0 ? RMAX : 1][kConsPix];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int p0 = blockIdx.x * kConsPix;
-  const int pix = p0 + lane;
-  const bool in = pix < npix;
-  if constexpr (RMAX > 0) {
-    for (int q = threadIdx.x; q < R * kConsPix; q += kBlock) {
-      const int r = q / kConsPix, l = q % kConsPix;
-      xn[r][l] = (p0 + l < npix) ? xext[(size_t)r * npix + p0 + l] : 0.0;
-    }
-    __syncthreads();
-  }
-  auto xrow = [&](int r) -> double {
-    if constexpr (RMAX > 0) return xn[r][lane];
-    return xext[(size_t)r * npix + pix];
-  };
-  const int P = gridDim.x;
-  constexpr int KU = 4;  // edges per wave whose y / z loads are in flight together
-  for (int eb0 = e0 + w; eb0 < e1; eb0 += 4 * KU) {
-    double yv[KU], zv[KU];
-#pragma unroll
-    for (int u = 0; u < KU; ++u) {
-      const int e = eb0 + 4 * u;
-      const bool ok = in && e < e1;
-      yv[u] = ok ? y[(size_t)e * npix + pix] : 0.0;
-      zv[u] = ok ? z[(size_t)e * npix + pix] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < KU; ++u) {
-      const int e = eb0 + 4 * u;
-      if (e >= e1) break;  // wave-uniform
-      double s[3] = {0.0, 0.0, 0.0};
-      if (in) {
-        const double xa = xrow(ea[e]), xb = xrow(eb[e]);
-        const double aa = xa + yv[u], ab = xb - yv[u];
-        const double zn = (aa + ab) * 0.5;
-        y[(size_t)e * npix + pix] = yv[u] + xa - zn;
-        z[(size_t)e * npix + pix] = zn;
-        const double ra = xa - zn, rb = xb - zn, dz = zn - zv[u];
-        s[0] = ra * ra;
-        s[1] = rb * rb;
-        s[2] = dz * dz;
-      }
-#pragma unroll
-      for (int q = 0; q < 3; ++q) s[q] = wave_sum_d(s[q]);
-      if (lane == 0) {
-#pragma unroll
-        for (int q = 0; q < 3; ++q) part[((size_t)e * 3 + q) * P + blockIdx.x] = s[q];
-      }
     }
   }
 }
