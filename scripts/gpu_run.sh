@@ -35,6 +35,9 @@ for step in "$@"; do
       mm=0; [ $step = sqm ] && mm=1
       ADMM_FWD_MIRROR=$mm PASSFILE=scripts/passes_fwd_sq.txt run $step 600 bash scripts/pmc.sh ${step}_${TAG} > gpurun_out/${step}_${TAG}.log 2>&1 || { tail -5 gpurun_out/${step}_${TAG}.log; exit 1; }
       python scripts/pmc_summary.py ${step}_${TAG} "k_fwdg<" "k_back" ;;
+    sq5)  # SQ counters (scripts/passes_sq_r5.txt: issue, LDS, wait, f64 / cvt counts) of the C3 headline, default modes
+      PASSFILE=scripts/passes_sq_r5.txt run sq5 600 bash scripts/pmc.sh sq5_${TAG} > gpurun_out/sq5_${TAG}.log 2>&1 || { tail -5 gpurun_out/sq5_${TAG}.log; exit 1; }
+      python scripts/pmc_summary.py sq5_${TAG} "k_fwdg<" "k_back_mirror<float, 8, 4, 3>" "k_tv_update<float, 4, false, true, true, true>" "k_cg_update<float, 4, true, false>" | tee gpurun_out/sq5_${TAG}_summary.txt ;;
     tests=*)
       expr=${step#tests=}
       if [ "$expr" = all ]; then k=(); else k=(-k "$expr"); fi
