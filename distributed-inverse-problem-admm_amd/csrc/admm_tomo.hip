@@ -953,11 +953,11 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
     const double kmn = C->Kb - c0 * (std::fabs(ba[t].Bi) + std::fabs(ba[t].Bj));
     C->kbias = std::max(C->kbias, (int)std::ceil(-kmn) + 2);
   }
-  if (C->wexp != 0) {  // exact power-of-two scaling (N < 3: L = 2 / (N |cos|) can exceed 1)
-    for (int t = 0; t < g.n_angles; ++t) {
-      bc[t].ws = float2v{std::ldexp(bc[t].ws.x, -C->wexp), std::ldexp(bc[t].ws.y, -C->wexp)};
-      bc[t].wc = float2v{std::ldexp(bc[t].wc.x, -C->wexp), std::ldexp(bc[t].wc.y, -C->wexp)};
-    }
+  // exact power-of-two scalings: 2^-wexp (N < 3: L = 2 / (N |cos|) can exceed 1) on ws and wc, and
+  // 2^-32 on ws, whose float taps multiply frac(k_f) x 2^32 (kernels.hpp kf_split)
+  for (int t = 0; t < g.n_angles; ++t) {
+    bc[t].ws = float2v{std::ldexp(bc[t].ws.x, -C->wexp - 32), std::ldexp(bc[t].ws.y, -C->wexp - 32)};
+    bc[t].wc = float2v{std::ldexp(bc[t].wc.x, -C->wexp), std::ldexp(bc[t].wc.y, -C->wexp)};
   }
   // angle groups for the grouped forward projector: consecutive angles of one case,
   // G <= kFgG, whose union row window of every block fits kFgWin (float64, same formulas as

@@ -62,6 +62,31 @@ struct alignas(32) BackAngleC {
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
 
+// Float back-projector taps take k_f + 2^20 (k_f in (0, 2^20): kbias makes it positive, N <= 4096
+// keeps it small), so the sum lies in [2^20, 2^21): its high dword is 0x41300000 + floor(k_f) and
+// its low dword is frac(k_f) x 2^32.  A tap then needs no v_fract_f64 / v_cvt_i32_f64 /
+// v_cvt_f32_f64: the weights take one v_cvt_f32_u32 of the low dword (the host scales the angle
+// records' ws by 2^-32) and the LDS address is one v_lshl_add of the high dword onto a window
+// offset stored with -0x41300000 x sizeof(sample vector) folded in (mod 2^32).  Position
+// resolution 2^-32 bin, the forward's 32.32 fixed point.
+constexpr double kKfBias = 1048576.0;
+constexpr unsigned kKfHi = 0x41300000u;
+__device__ __forceinline__ void kf_split(double kfb, unsigned& hi, float& fu) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, kfb);
+  hi = (unsigned)(b >> 32);
+  fu = (float)(unsigned)b;  // frac(k_f) x 2^32
+}
+// hi x PB + koff in one v_lshl_add_u32 (written out: the compiler forms hi << 4 from the 64-bit
+// value by a funnel shift, a mask and an add); PB = the window's sample-vector bytes
+template <int PB>
+__device__ __forceinline__ int kf_addr(unsigned hi, int koff) {
+  static_assert(PB == 4 || PB == 8 || PB == 16 || PB == 32, "power-of-two sample vectors");
+  constexpr int SH = PB == 4 ? 2 : PB == 8 ? 3 : PB == 16 ? 4 : 5;
+  int off;
+  asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(off) : "v"(hi), "i"(SH), "v"(koff));
+  return off;
+}
+
 // ---------------------------------------------------------------------------
 // vector I/O of VB samples (VB*sizeof(T) contiguous bytes)
 // ---------------------------------------------------------------------------
@@ -1417,6 +1442,8 @@ void k_back(BackArgs<T> A) {
   // offsets and the staged bins take the same bias
   const int kbias = A.kbias;
   const double Kc = A.K + (double)kbias;
+  const double Kcb = Kc + kKfBias;  // (float taps, kf_split)
+  constexpr bool FB = std::is_same<T, float>::value;  // biased window offsets (kf_split)
 
   // angles per staged chunk: halved for 64-B sample vectors (8 float64 nodes) so the
   // window stays at 48 KB of LDS
@@ -1438,30 +1465,37 @@ void k_back(BackArgs<T> A) {
   constexpr int PB = (int)sizeof(Pack<T, PV>);
   auto tap = [&](const BackAngleC& g, int koff, T& w0, T& w1, Pack<T, PV> (&s0)[NPL], Pack<T, PV> (&s1)[NPL],
                  int tt) {
-    const double kf = fma(xi, g.Bi, fma(yj, g.Bj, Kc));
-    const int k0 = (int)kf;  // == floor(kf): kf > 0
-    const T f = (T)__builtin_amdgcn_fract(kf);
+    int k0, off;
     if constexpr (std::is_same<T, float>::value) {
       // one v_pk_fma_f32 for both taps (bitwise the two scalar fmas: f * (-sL) == (-f) * sL)
       // wc to VGPRs by one v_mov_b64 (the compiler emits two v_mov_b32; VOP3P reads one SGPR
       // pair).  max(0, w) is the fma's clamp to [0, 1]: the host scales ws, wc by 2^-wexp so
       // that w <= L 2^-wexp <= 1 (wexp = 0 for N >= 3), undone exactly after the angle loop
+      unsigned hi;
       float2v wc, fv, w;
+      float fu;
+      kf_split(fma(xi, g.Bi, fma(yj, g.Bj, Kcb)), hi, fu);  // (fu: frac x 2^32; ws carries 2^-32)
+      fv.x = fu;  // op_sel_hi:[0,...] reads the low half for both lanes of the pair
       asm("v_mov_b64 %0, %1" : "=v"(wc) : "s"(g.wc));
-      fv.x = f;  // op_sel_hi:[0,...] reads the low half for both lanes of the pair
       asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] clamp" : "=v"(w) : "v"(fv), "s"(g.ws), "v"(wc));
       w0 = w.x;
       w1 = w.y;
+      k0 = (int)(hi - kKfHi);
+      off = kf_addr<PB>(hi, koff);  // (koff carries -kKfHi x PB)
     } else {
+      const double kf = fma(xi, g.Bi, fma(yj, g.Bj, Kc));
+      k0 = (int)kf;  // == floor(kf): kf > 0
+      const T f = (T)__builtin_amdgcn_fract(kf);
       const BackAngle& gd = A.ang[t0c + tt];
       w0 = fmax(T(0), T(1) - f * (T)gd.slope) * (T)gd.L;
       w1 = fmax(T(0), T(1) - (T(1) - f) * (T)gd.slope) * (T)gd.L;
+      off = k0 * PB + koff;
     }
     if constexpr (MODE == BACK_WSQ) {
+      (void)off;
       w0 = (k0 >= kbias && k0 <= kbias + n_det - 1) ? w0 : T(0);
       w1 = (k0 >= kbias - 1 && k0 <= kbias + n_det - 2) ? w1 : T(0);
     } else {
-      const int off = k0 * PB + koff;
 #pragma unroll
       for (int q = 0; q < NPL; ++q) {
         const char* wb = reinterpret_cast<const char*>(&win[q][0][0]) + off;
@@ -1508,7 +1542,8 @@ void k_back(BackArgs<T> A) {
     // vmcnt(0) -- which would also wait for the window prefetch issued before it
     auto kf = [&](int ii, int jj) { return fma((double)ii - c0, bij.x, fma((double)jj - c0, bij.y, Kc)); };
     const double kmn = fmin(fmin(kf(ib, jb), kf(ib, jhi)), fmin(kf(ihi, jb), kf(ihi, jhi)));
-    const int koff = ((int)threadIdx.x * kBWin - ((int)floor(kmn) - 1)) * PB;
+    int koff = ((int)threadIdx.x * kBWin - ((int)floor(kmn) - 1)) * PB;
+    if constexpr (FB) koff = (int)((unsigned)koff - kKfHi * (unsigned)PB);  // (kf_split)
     // unmasked store (threads past the chunk's angles write slots no tap reads, or the spare
     // one): a masked store lets the compiler sink the whole computation under the mask
     reinterpret_cast<int*>(kmin_s[buf])[min((int)threadIdx.x, ANGC)] = koff;
@@ -1522,7 +1557,9 @@ void k_back(BackArgs<T> A) {
       const int q = threadIdx.x + e * kBkThreads;
       const int pl = q % NPL, aw = q / NPL;
       const int a = aw / kBWin, w = aw - a * kBWin;
-      const int k = (a < nt) ? a * kBWin - reinterpret_cast<const int*>(kmin_s[buf])[a] / PB + w - kbias : -1;
+      int ko = (a < nt) ? reinterpret_cast<const int*>(kmin_s[buf])[a] : 0;
+      if constexpr (FB) ko = (int)((unsigned)ko + kKfHi * (unsigned)PB);  // the unbiased offset
+      const int k = (a < nt) ? a * kBWin - ko / PB + w - kbias : -1;
       if (a < nt && k >= 0 && k < n_det) {
         wst[e] = *reinterpret_cast<const Pack<T, PV>*>(sino_c + ((size_t)(t0 + a) * n_det + k) * VB + pl * PV);
       } else {
@@ -1705,6 +1742,8 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
   const int jhi = min(jb + kBTJ - 1, N - 1), ihi = min(ib + kBTI - 1, Nh - 1);
   const int kbias = A.kbias;
   const double Kc = A.K + (double)kbias;
+  const double Kcb = Kc + kKfBias;  // (float taps, kf_split)
+  constexpr bool FB = std::is_same<T, float>::value;  // biased window offsets (kf_split)
   constexpr int ANGC_ = ((NPL > 2) ? kBAngC / 2 : kBAngC) / 2;
   constexpr int ANGC_DIAG = (98304 / (2 * NPL * kBWin * PB)) & ~3;
   constexpr int ANGC = (MODE == BACK_DIAG && ANGC_ > ANGC_DIAG) ? ANGC_DIAG : ANGC_;
@@ -1731,7 +1770,8 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
     auto kf = [&](double xx, int jj) { return fma(xx, bij.x, fma((double)jj - c0, bij.y, Kc)); };
     const double kmn = fmin(fmin(kf(x0, jb), kf(x0, jhi)), fmin(kf(x1, jb), kf(x1, jhi)));
     const int a = (int)threadIdx.x % ANGC;
-    const int koff = (a * kBWin - ((int)floor(kmn) - 1)) * PB;
+    int koff = (a * kBWin - ((int)floor(kmn) - 1)) * PB;
+    if constexpr (FB) koff = (int)((unsigned)koff - kKfHi * (unsigned)PB);  // (kf_split)
     reinterpret_cast<int*>(kmin_s[buf][min(w, 1)])[w < 2 ? a : ANGC] = koff;  // (spare slot)
   };
   auto kmin_chunk = [&](int t0, int buf) { kmin_store(buf, kmin_load(t0)); };
@@ -1746,7 +1786,9 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
       const int pl = q % NPL, rest = q / NPL, bin = rest % kBWin, aw = rest / kBWin;
       const int a = aw % ANGC, w = aw / ANGC;
       const bool live = q < NE && a < nt;
-      const int k = live ? a * kBWin - reinterpret_cast<const int*>(kmin_s[buf][w])[a] / PB + bin - kbias : -1;
+      int ko = live ? reinterpret_cast<const int*>(kmin_s[buf][w])[a] : 0;
+      if constexpr (FB) ko = (int)((unsigned)ko + kKfHi * (unsigned)PB);  // the unbiased offset
+      const int k = live ? a * kBWin - ko / PB + bin - kbias : -1;
       const int t = t0 + a;
       const size_t ray0 = (size_t)t * n_det + k, ray1 = (size_t)(2 * n_ang - 1 - t) * n_det + k;
       if (live && k >= 0 && k < n_det) {
@@ -1772,26 +1814,31 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
       if (q < NE && a < nt) win[w][pl][a][bin] = wst[e];
     }
   };
-  // one angle's taps of one pixel from window W (k_back's tap)
+  // one angle's taps of one pixel from window W (k_back's tap; float: kf is biased, kf_split)
   auto tap1 = [&](auto wc_, const BackAngleC& g, double kf, int koff, int tt, T(&acc)[VB]) {
     constexpr int w = decltype(wc_)::value;
     {
-      const int k0 = (int)kf;  // == floor(kf): kf > 0
-      const T f = (T)__builtin_amdgcn_fract(kf);
       T w0, w1;
+      int off;
       if constexpr (std::is_same<T, float>::value) {
+        unsigned hi;
         float2v wc, fv, ww;
+        float fu;
+        kf_split(kf, hi, fu);
+        fv.x = fu;
         asm("v_mov_b64 %0, %1" : "=v"(wc) : "s"(g.wc));
-        fv.x = f;
         asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] clamp" : "=v"(ww) : "v"(fv), "s"(g.ws), "v"(wc));
         w0 = ww.x;
         w1 = ww.y;
+        off = kf_addr<PB>(hi, koff);  // (koff carries -kKfHi x PB)
       } else {
+        const int k0 = (int)kf;  // == floor(kf): kf > 0
+        const T f = (T)__builtin_amdgcn_fract(kf);
         const BackAngle& gd = A.ang[t0c + tt];
         w0 = fmax(T(0), T(1) - f * (T)gd.slope) * (T)gd.L;
         w1 = fmax(T(0), T(1) - (T(1) - f) * (T)gd.slope) * (T)gd.L;
+        off = k0 * PB + koff;
       }
-      const int off = k0 * PB + koff;
 #pragma unroll
       for (int q = 0; q < NPL; ++q) {
         const char* wb = reinterpret_cast<const char*>(&win[w][q][0][0]) + off;
@@ -1807,7 +1854,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
   };
   // both pixels: kf at xi and at -xi (the mirror pixel), sharing the j term
   auto tap2 = [&](const BackAngleC& g, int koff1, int koff2, int tt) {
-    const double inner = fma(yj, g.Bj, Kc);
+    const double inner = fma(yj, g.Bj, FB ? Kcb : Kc);
     tap1(std::integral_constant<int, 0>{}, g, fma(xi, g.Bi, inner), koff1, tt, acc1);
     tap1(std::integral_constant<int, 1>{}, g, fma(-xi, g.Bi, inner), koff2, tt, acc2);
   };
