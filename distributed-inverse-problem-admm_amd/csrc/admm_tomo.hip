@@ -455,7 +455,9 @@ int launch_fwd_batch(admm_ctx* C, const T* img, const T* imgT, T* sino, const T*
   if (C->mm) {  // virtual partials -> the real sinogram (both angles of every virtual ray)
     constexpr int VBV = mirror_vb<T, VB>(), MH = VBV / 2;
     const int mh = C->half->mrays;
-    dim3 mg((mh + kBlock - 1) / kBlock, nch * (VB / MH));
+    // MODE 0: two threads per virtual ray (k_fwd_combine_mirror); MODE 1: one (its block partials)
+    const size_t mthreads = (size_t)mh * (MODE == 0 ? 2 : 1);
+    dim3 mg((unsigned)((mthreads + kBlock - 1) / kBlock), nch * (VB / MH));
     hipLaunchKernelGGL((k_fwd_combine_mirror<T, VBV, VB, MODE>), mg, dim3(kBlock), 0, s, (const T*)C->fpart.p, sino,
                        b, part, C->half->fang, C->g.n_det, C->half->g.n_angles, V);
     CHECK_LAUNCH();

@@ -1039,6 +1039,30 @@ __global__ __launch_bounds__(kBlock) void k_fwd_combine_mirror(const T* __restri
   const int rc = chunk / MS, mq = chunk % MS;     // real chunk, lane block
   const int vr0 = rc * VBR + mq * MH;             // first real node of the lane block
   const size_t m_half = (size_t)n_ang_half * n_det, m_full = 2 * m_half;
+  if constexpr (MODE == 0) {
+    // two adjacent threads per virtual ray: lanes < VB/2 (-> angle t) and lanes >= VB/2 (-> angle
+    // a-1-t), each summing its half over the segments in the same order as below (same bits),
+    // twice the loads in flight of a thread-per-ray grid (grid.x doubled by the launcher)
+    const size_t q = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t ray = q >> 1;
+    const int h = (int)(q & 1);
+    if (ray >= m_half) return;
+    const int t = (int)(ray / n_det), k = (int)(ray % n_det);
+    const T L = (T)ang[t].L;
+    T acc[MH], pv[MH];
+    gload<T, MH>(part + ((size_t)chunk * m_half + ray) * VB + h * MH, acc);
+#pragma unroll
+    for (int sg = 1; sg < kFgSeg; ++sg) {
+      gload<T, MH>(part + (((size_t)sg * nch + chunk) * m_half + ray) * VB + h * MH, pv);
+#pragma unroll
+      for (int u = 0; u < MH; ++u) acc[u] += pv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < MH; ++u) acc[u] *= L;
+    const size_t dst = h ? (size_t)(2 * n_ang_half - 1 - t) * n_det + k : ray;
+    gstore<T, MH>(sino + (size_t)rc * m_full * VBR + mq * MH + dst * VBR, acc);
+    return;
+  }
   const size_t ray = (size_t)blockIdx.x * kBlock + threadIdx.x;
   double sq[MH];
 #pragma unroll
@@ -1201,10 +1225,11 @@ __device__ __forceinline__ double kt_w_at(const double* __restrict__ d, const do
   return s;
 }
 
-// Fused epilogue of one pixel: writes the mode's per-pixel outputs and adds the
-// pixel's reduction terms into pq.
+// Fused epilogue of one pixel: writes the mode's per-pixel outputs and stores the pixel's
+// reduction terms into pq (ACC: adds them, the second pixel of a mirror pair; the caller
+// zero-fills pq, so out-of-image pixels and dead lanes contribute 0).
 // VS / lo (mirror mode): the VB lanes handled are lanes lo .. lo+VB-1 of VS-lane sample vectors.
-template <typename T, int VB, int MODE, int NQ, int VS = VB>
+template <typename T, int VB, int MODE, int NQ, int VS = VB, bool ACC = false>
 __device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j, int chunk, int v0, int nv,
                                               const T (&acc)[VB], double (&pq)[VB][NQ], int lo = 0) {
   const int N = A.N;
@@ -1225,12 +1250,13 @@ __device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j
     T pc[VB], pn[VB];
     double ktk[VB];
     gload<T, VB>(pv + (size_t)pix * VS, pc);
-#pragma unroll
-    for (int u = 0; u < VB; ++u) ktk[u] = 0.0;
-    if (i >= 1) {
+    if (i >= 1) {  // (the first term assigned: no 0 + x)
       gload<T, VB>(pv + (size_t)(pix - N) * VS, pn);
 #pragma unroll
-      for (int u = 0; u < VB; ++u) ktk[u] += (double)pc[u] - (double)pn[u];
+      for (int u = 0; u < VB; ++u) ktk[u] = (double)pc[u] - (double)pn[u];
+    } else {
+#pragma unroll
+      for (int u = 0; u < VB; ++u) ktk[u] = 0.0;
     }
     if (i <= N - 2) {
       gload<T, VB>(pv + (size_t)(pix + N) * VS, pn);
@@ -1264,11 +1290,19 @@ __device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j
           outv[u] = hp;
           const double hd = (double)hp;
           const double rv = A.r[vo + pix];
-          pq[u][0] += pcd * hd;
-          pq[u][1] += rv * hd;
-          pq[u][2] += hd * hd;
-          pq[u][3] += rv * rv;
-          pq[u][4] += rv * pcd;
+          if constexpr (ACC) {  // the mirror pixel of a pair: onto the first pixel's terms
+            pq[u][0] += pcd * hd;
+            pq[u][1] += rv * hd;
+            pq[u][2] += hd * hd;
+            pq[u][3] += rv * rv;
+            pq[u][4] += rv * pcd;
+          } else {
+            pq[u][0] = pcd * hd;
+            pq[u][1] = rv * hd;
+            pq[u][2] = hd * hd;
+            pq[u][3] = rv * rv;
+            pq[u][4] = rv * pcd;
+          }
         } else {
           const double* dv = A.dvar + 2 * vo;
           const double* ev = A.evar + 2 * vo;
@@ -1921,7 +1955,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
     diag_epilogue_tile<T, MH, VBR>(A, diag_s, N - ib - kBTI, jb, i2, j, inb2, rc, v0, nv, r2, pq, mq * MH);
   } else {
     if (inb) back_epilogue<T, MH, MODE, NQ, VBR>(A, i, j, rc, v0, nv, r1, pq, mq * MH);
-    if (inb2) back_epilogue<T, MH, MODE, NQ, VBR>(A, i2, j, rc, v0, nv, r2, pq, mq * MH);
+    if (inb2) back_epilogue<T, MH, MODE, NQ, VBR, true>(A, i2, j, rc, v0, nv, r2, pq, mq * MH);
   }
   if constexpr (MODE == BACK_H || MODE == BACK_DIAG) {
     constexpr int NV = ((MH * NQ + 15) / 16) * 16;
