@@ -240,7 +240,7 @@ def cpu_baseline(N, a, b, q, x_gpu, procs=None, budget=CPU_BASELINE_SECONDS):
 # MI355X_MICROARCH.md gfx950 correction), one per headline workload: the per-launch
 # figure depends on the node chunks one launch projects.  PMC counters cannot be read
 # inside this run.
-TRAFFIC_FILES = {"C3": "profiles/r4_traffic.json", "weak8": "profiles/r4_traffic_weak8.json"}
+TRAFFIC_FILES = {"C3": "profiles/r5_traffic.json", "weak8": "profiles/r5_traffic_weak8.json"}
 
 
 def fwd_kernel_traffic(tr, tname, vb, mirror):
