@@ -69,7 +69,12 @@ class ShardPlan:
         return len(self.local_nodes) + len(self.halo_nodes)
 
     def use_allgather(self) -> bool:
-        """All-gather when some rank needs most of its remote images (dense / ER graphs).
+        """All-gather only when it moves no more bytes to the busiest rank than p2p would:
+        an all-gather lands (world - 1) x vmax images on every rank, the grouped p2p exactly
+        a rank's halo rows, so p2p wins unless some rank needs (nearly) every remote image --
+        complete graphs (C5).  C4's 32-node ER graph on 8 ranks: at most 20 halo rows against
+        28 all-gathered images per rank.  (Round 4's rule all-gathered whenever a rank needed
+        more than half its remote images.)
 
         The exchange is a collective, so the choice is made from the whole graph and node
         partition -- the same on every rank (a rank-local choice let C4's 32-node ER graph
@@ -87,10 +92,9 @@ class ShardPlan:
                 if ra != rb:
                     halo[ra].add(b)
                     halo[rb].add(a)
-            cached = False
-            for r, (lo, hi) in enumerate(self.ranges):
-                remote = self.V_total - (hi - lo)
-                cached = cached or (remote > 0 and len(halo[r]) * 2 > remote)
+            vmax = max(hi - lo for lo, hi in self.ranges)
+            busiest = max(len(h) for h in halo)
+            cached = busiest > 0 and busiest >= (self.world - 1) * vmax
             self.__dict__["_allgather"] = cached
         return cached
 

@@ -85,13 +85,14 @@ def test_bench_config_line(cuda):
 def test_bench_as_rank_share(cuda):
     """``--config C4 --as-rank 0/8``: rank 0's share of C4 on 8 GPUs bound on this GPU --
     4 local nodes (one batch at node-interleave width 4), its real halo rows and stored
-    edges of the 103-edge ER graph, all-gather exchange priced, not run."""
+    edges of the 103-edge ER graph, its p2p halo exchange priced, not run."""
     b = _run("--config", "C4", "--as-rank", "0/8", "--steps", "2", "--warmup", "1")
     sh = b["share"]
     assert b["unit"] == "ms/step" and b["value"] == sh["ms_per_step"] > 0
     assert sh["local_nodes"] == 4 and sh["vb"] == 4 and sh["batches"] == 1 and sh["rank"] == 0
     assert sh["halo_rows"] > 0 and sh["stored_edges"] > 0
-    assert sh["exchange"]["mode"] == "allgather" and sh["exchange"]["bytes_received"] == 7 * 4 * 1024 * 1024 * 8
+    assert sh["exchange"]["mode"] == "p2p"
+    assert sh["exchange"]["bytes_received"] == sh["halo_rows"] * 1024 * 1024 * 8
 
 
 @pytest.mark.timeout(600)

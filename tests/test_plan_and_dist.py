@@ -52,8 +52,11 @@ def test_exchange_mode_is_the_same_on_every_rank(world):
             continue
         modes = {make_plan(G, V, world, r).use_allgather() for r in range(world)}
         assert len(modes) == 1, (name, world)
+    # the byte-minimising rule: ER graphs exchange halo rows point to point (C4@8: at most 21
+    # halo rows against 28 all-gathered images), complete graphs all-gather
     G = dict(scale_graphs())["er32"]
-    assert make_plan(G, 32, 8, 0).use_allgather()
+    assert not make_plan(G, 32, 8, 0).use_allgather()
+    assert make_plan(nx.complete_graph(64), 64, 8, 0).use_allgather()
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 4])
@@ -240,7 +243,8 @@ def run_sharded(rank, world, gname, HaloExchange, assemble_stats, gather_images,
 
 
 # world 2: both halo directions go to the same peer; world 4 on the ring: distinct left and
-# right peers (the 8-GPU layout), on the ER graph an uneven 3/2/2/2 split and the all-gather
+# right peers (the 8-GPU layout), on the ER graph an uneven 3/2/2/2 split with p2p to several
+# peers; the complete graph all-gathers
 @pytest.mark.parametrize("gname,world", [("ring8", 2), ("complete6", 2), ("er9", 2), ("ring8", 4), ("er9", 4)])
 def test_gloo_sharded_matches_single_process_bitwise(gname, world):
     from admm_hip.exchange import HaloExchange, assemble_stats, gather_images
@@ -275,7 +279,7 @@ def test_gloo_sharded_matches_single_process_bitwise(gname, world):
 @pytest.mark.parametrize("gname,world", [("er9", 4), ("ring8", 4), ("complete6", 2)])
 def test_gloo_overlapped_exchange_matches_serial_bitwise(gname, world):
     """RankGroups.exchange_consensus's order (rank-internal edges updated while the halo images
-    are in flight: asynchronous all-gather on ER / complete graphs, p2p on the ring) gives the
+    are in flight: asynchronous all-gather on the complete graph, p2p on the ring and ER) gives the
     serial exchange-then-consensus run bitwise, and the single-process run."""
     from admm_hip.exchange import HaloExchange, assemble_stats, gather_images
     X1, h1 = run_sharded(0, 1, gname, HaloExchange, assemble_stats, gather_images, make_plan)
