@@ -59,6 +59,21 @@ def test_exchange_mode_is_the_same_on_every_rank(world):
     assert make_plan(nx.complete_graph(64), 64, 8, 0).use_allgather()
 
 
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_exchange_mode_minimises_the_busiest_ranks_bytes(world):
+    """The chosen halo exchange lands no more images on the busiest rank than the other mode
+    would: all-gather (world - 1) x vmax per rank, p2p a rank's halo rows."""
+    for name, G in list(graphs()) + list(scale_graphs()):
+        V = G.number_of_nodes()
+        if V < world:
+            continue
+        plans = [make_plan(G, V, world, r) for r in range(world)]
+        vmax = max(hi - lo for lo, hi in plans[0].ranges)
+        ag, p2p = (world - 1) * vmax, max(len(p.halo_nodes) for p in plans)
+        chosen = ag if plans[0].use_allgather() else p2p
+        assert chosen <= min(ag, p2p), (name, world, ag, p2p)
+
+
 @pytest.mark.parametrize("world", [1, 2, 3, 4])
 def test_plan_partitions_nodes_and_edges(world):
     for name, G in graphs():
