@@ -53,7 +53,10 @@ def rel(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
 
 
-CFG = {"C4": dict(N=1024, V=32, graph="er", dtype="float32", tv="iso", iters=2),
+# (ADMM_TEST_C4_ITERS: a longer C4 trajectory for a one-off run; the suite keeps 2 for its time
+# budget -- profiles/r5_pytest_c4_full_5iter.log holds a 5-iteration run)
+CFG = {"C4": dict(N=1024, V=32, graph="er", dtype="float32", tv="iso",
+                  iters=int(os.environ.get("ADMM_TEST_C4_ITERS", "2"))),
        "C5": dict(N=2048, V=64, graph="complete", dtype="float64", tv="aniso", iters=1)}
 
 
@@ -160,8 +163,21 @@ def test_c4_full_graph_matches_operator_oracle(cuda):
     assert chk["worst"] < 1e-12, chk
     r2 = _run("C4")  # bitwise repeatable
     _same(r1, r2)
-    xo, ho = oadmm.decentralized_admm(ops, r1["sinos"], G, Q, c["N"], lam_tv=0.02, rho=2.0,
-                                      max_iters=c["iters"], eps_pri=0.0, eps_dual=0.0, phantom_true=ph)
+    import threading
+    stop = threading.Event()
+
+    def beat():  # a progress line a minute: the operator-level oracle runs minutes per iteration
+        t = 0
+        while not stop.wait(60):
+            t += 60
+            print(f"C4 oracle running, {t} s", flush=True)
+    hb = threading.Thread(target=beat, daemon=True)
+    hb.start()
+    try:
+        xo, ho = oadmm.decentralized_admm(ops, r1["sinos"], G, Q, c["N"], lam_tv=0.02, rho=2.0,
+                                          max_iters=c["iters"], eps_pri=0.0, eps_dual=0.0, phantom_true=ph)
+    finally:
+        stop.set()
     h = r1["hist"]
     errs = {"x": rel(r1["x"], np.stack(xo)), "primal": rel(h["primal"], ho["primal"]),
             "dual": rel(h["dual"], ho["dual"]), "obj": rel(h["obj_total"], ho["obj_total"])}
@@ -174,7 +190,7 @@ def test_c4_full_graph_matches_operator_oracle(cuda):
 @pytest.mark.parametrize("world", [4, 8])
 def test_c4_ranks_match_one_rank_bitwise(cuda, world):
     """C4 sharded over 4 and over 8 ranks (its 8-GPU layout: 4 nodes per rank, node
-    interleave 4, all-gather exchange chosen on every rank) bitwise equal to one process."""
+    interleave 4, p2p halo exchange chosen on every rank) bitwise equal to one process."""
     r1 = _spawn("C4", 1, 500)[0]
     res = _spawn("C4", world, 700)
     for r in range(world):
