@@ -543,6 +543,21 @@ struct FgRange {
   int nk[kFgG];
 };
 
+// The float forward keeps its tap weights in the units of its 32.32 fixed-point positions
+// (w1 = the fraction's low word as a float, w0 = 2^32 - w1: one VALU less per tap row than
+// scaling each fraction by 2^-32), so its segment partials carry a factor 2^32 that the
+// combines fold into L (kFgWScale).  Power-of-two scalings commute with rounding (no overflow
+// or underflow at these magnitudes): every partial, sum and A x is bitwise what the unscaled
+// weights gave.
+template <typename T>
+constexpr T kFgWOne = T(1);
+template <>
+constexpr float kFgWOne<float> = 4294967296.0f;
+template <typename T>
+constexpr T kFgWScale = T(1);
+template <>
+constexpr float kFgWScale<float> = 2.3283064365386963e-10f;
+
 #ifndef ADMM_FG_WPE
 #define ADMM_FG_WPE 8  // waves per SIMD the register budget must allow: <= 64 VGPRs, 2 blocks/CU
                        // (float64 samples otherwise take 67 and fall to one block per CU)
@@ -684,7 +699,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       T w1;
       if constexpr (std::is_same<T, float>::value) {
         idx = (int)(lfix >> 32) - wl[r];
-        w1 = (float)(unsigned)lfix * 2.3283064365386963e-10f;  // fraction * 2^-32
+        w1 = (float)(unsigned)lfix;  // fraction x 2^32 (kFgWScale<float>)
         lfix += dlfix;
       } else {
         const double l = fma((double)(m0 + r), a.dl, l0);
@@ -692,7 +707,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         idx = (int)fl - wl[r];
         w1 = (T)(l - fl);
       }
-      const T w0 = T(1) - w1;
+      const T w0 = kFgWOne<T> - w1;
       // taps idx (weight w0) and idx+1 (w1): one is even, one odd
       const bool odd = idx & 1;
       const int se = (idx + 1) >> 1, so = kFgOdd + (idx >> 1);
@@ -722,7 +737,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       T w1;
       if constexpr (std::is_same<T, float>::value) {
         idx = (int)(lfix >> 32) - wl_cur[r];
-        w1 = (float)(unsigned)lfix * 2.3283064365386963e-10f;
+        w1 = (float)(unsigned)lfix;  // fraction x 2^32 (kFgWScale<float>)
         lfix += dlfix;
       } else {
         const double l = fma((double)(m0 + r), a.dl, l0);
@@ -730,7 +745,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         idx = (int)fl - wl_cur[r];
         w1 = (T)(l - fl);
       }
-      const T w0 = T(1) - w1;
+      const T w0 = kFgWOne<T> - w1;
       se[r] = (idx + 1) >> 1;
       so[r] = kFgOdd + (idx >> 1);
       if constexpr (std::is_same<T, float>::value) {
@@ -989,7 +1004,7 @@ __global__ __launch_bounds__(kBlock) void k_fwd_combine(const T* __restrict__ pa
 #pragma unroll
   for (int u = 0; u < VB; ++u) sq[u] = 0.0;
   if (ray < m_rays) {
-    const T L = (T)ang[ray / n_det].L;
+    const T L = (T)ang[ray / n_det].L * kFgWScale<T>;
     T acc[VB], pv[VB];
     gload<T, VB>(part + ((size_t)chunk * m_rays + ray) * VB, acc);
 #pragma unroll
@@ -1048,7 +1063,7 @@ __global__ __launch_bounds__(kBlock) void k_fwd_combine_mirror(const T* __restri
     const int h = (int)(q & 1);
     if (ray >= m_half) return;
     const int t = (int)(ray / n_det), k = (int)(ray % n_det);
-    const T L = (T)ang[t].L;
+    const T L = (T)ang[t].L * kFgWScale<T>;
     T acc[MH], pv[MH];
     gload<T, MH>(part + ((size_t)chunk * m_half + ray) * VB + h * MH, acc);
 #pragma unroll
@@ -1070,7 +1085,7 @@ __global__ __launch_bounds__(kBlock) void k_fwd_combine_mirror(const T* __restri
   if (ray < m_half) {
     const int t = (int)(ray / n_det), k = (int)(ray % n_det);
     const size_t ray2 = (size_t)(2 * n_ang_half - 1 - t) * n_det + k;  // angle a-1-t
-    const T L = (T)ang[t].L;
+    const T L = (T)ang[t].L * kFgWScale<T>;
     T acc[VB], pv[VB];
     gload<T, VB>(part + ((size_t)chunk * m_half + ray) * VB, acc);
 #pragma unroll
