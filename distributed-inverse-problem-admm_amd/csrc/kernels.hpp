@@ -729,7 +729,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   // flight behind the other's arithmetic (the LDS-DMA staging freed the registers: the
   // register-staged kernel had no room for the second row's 16).  Same FMAs, same order.
   auto taps4 = [&](const Pack<T, PV> (&wb)[NPL][R][kFgRow], int m0) {
-    int se[R], so[R];
+    int se[R], so[R];  // (float: byte offsets of the even / odd slot; else slot indices)
     T we[R], wo[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -746,12 +746,14 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         w1 = (T)(l - fl);
       }
       const T w0 = kFgWOne<T> - w1;
-      se[r] = (idx + 1) >> 1;
-      so[r] = kFgOdd + (idx >> 1);
       if constexpr (std::is_same<T, float>::value) {
         // parity mask (0 / -1) and two bitfield selects: 3 VALU instead of and + compare +
         // 2 conditional moves (same values, bit for bit)
         const int msk = __builtin_amdgcn_sbfe(idx, 0, 1);
+        // slot byte offsets: odd (idx >> 1) x 16, even ceil(idx / 2) x 16 = odd - 16 msk (one
+        // v_mad_i32_i24 on the mask instead of a shift-add and a mask of its own)
+        so[r] = (idx >> 1) << 4;
+        asm("v_mad_i32_i24 %0, %1, -16, %2" : "=v"(se[r]) : "v"(msk), "v"(so[r]));
         const int i0 = __float_as_int(w0), i1 = __float_as_int(w1);
         int ie, io;
         asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(ie) : "v"(msk), "v"(i1), "v"(i0));
@@ -759,24 +761,35 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         we[r] = __int_as_float(ie);
         wo[r] = __int_as_float(io);
       } else {
+        se[r] = (idx + 1) >> 1;
+        so[r] = kFgOdd + (idx >> 1);
         const bool odd = idx & 1;
         we[r] = odd ? w1 : w0;
         wo[r] = odd ? w0 : w1;
       }
     }
+    // the even / odd tap samples of row r, plane q
+    auto slot = [&](int q, int r, bool even) -> Pack<T, PV> {
+      if constexpr (std::is_same<T, float>::value) {
+        const char* row = reinterpret_cast<const char*>(&wb[q][r][0]);
+        return *reinterpret_cast<const Pack<T, PV>*>(even ? row + se[r] : row + kFgOdd * (int)sizeof(Pack<T, PV>) + so[r]);
+      } else {
+        return wb[q][r][even ? se[r] : so[r]];
+      }
+    };
     Pack<T, PV> cur[2 * NPL], nxt[2 * NPL];
 #pragma unroll
     for (int q = 0; q < NPL; ++q) {
-      cur[2 * q] = wb[q][0][se[0]];
-      cur[2 * q + 1] = wb[q][0][so[0]];
+      cur[2 * q] = slot(q, 0, true);
+      cur[2 * q + 1] = slot(q, 0, false);
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (r + 1 < R) {
 #pragma unroll
         for (int q = 0; q < NPL; ++q) {
-          nxt[2 * q] = wb[q][r + 1][se[r + 1]];
-          nxt[2 * q + 1] = wb[q][r + 1][so[r + 1]];
+          nxt[2 * q] = slot(q, r + 1, true);
+          nxt[2 * q + 1] = slot(q, r + 1, false);
         }
       }
 #pragma unroll
