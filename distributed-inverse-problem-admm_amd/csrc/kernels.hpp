@@ -1934,10 +1934,11 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
     if (t0 + ANGC < n_ang) wfetch(t0 + ANGC, kb ^ 1);  // in flight during this chunk's taps
     t0c = t0;
     int tt = 0;
-    for (; tt + 4 <= nt; tt += 4) {
+    const BackAngleC* gq = A.angc + t0;  // (records at non-negative immediate offsets of one base)
+    for (; tt + 4 <= nt; tt += 4, gq += 4) {
       BackAngleC g[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) g[u] = A.angc[t0 + tt + u];
+      for (int u = 0; u < 4; ++u) g[u] = gq[u];
       const int4 k1 = kmin_s[kb][0][tt >> 2], k2 = kmin_s[kb][1][tt >> 2];
       tap2(g[0], k1.x, k2.x, tt);
       tap2(g[1], k1.y, k2.y, tt + 1);
