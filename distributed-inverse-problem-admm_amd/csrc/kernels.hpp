@@ -1687,10 +1687,11 @@ void k_back(BackArgs<T> A) {
     // run on LDS reads alone
     t0c = t0;
     int tt = 0;
-    for (; tt + 4 <= nt; tt += 4) {
+    const BackAngleC* gq = A.angc + t0;  // (records at non-negative immediate offsets of one base)
+    for (; tt + 4 <= nt; tt += 4, gq += 4) {
       BackAngleC g[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) g[u] = A.angc[t0 + tt + u];
+      for (int u = 0; u < 4; ++u) g[u] = gq[u];
       int4 km = make_int4(0, 0, 0, 0);
       if constexpr (MODE != BACK_WSQ) km = kmin_s[kb][tt >> 2];
       const int kms[4] = {km.x, km.y, km.z, km.w};
