@@ -1841,6 +1841,15 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
   constexpr int NE = 2 * ANGC * kBWin * NPL;  // staged packs per chunk
   constexpr int SPER = (NE + kBkThreads - 1) / kBkThreads;
   Pack<T, PV> wst[SPER];
+  // (16-byte planes: the window bins as buffer loads at 32-bit offsets from one scalar base; a
+  // bin outside the detector is an out-of-range offset, zero-filled by the hardware)
+  constexpr bool WBUF = NPL == 2 && sizeof(Pack<T, PV>) == 16;
+  const __amdgpu_buffer_rsrc_t rs_sino = [&] {
+    const uint64_t b = (uint64_t)(uintptr_t)sino_c;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    return make_rsrc((const void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (uint32_t)(m_full * VBR * sizeof(T)));
+  }();
   auto wfetch = [&](int t0, int buf) {
     const int nt = min(ANGC, n_ang - t0);
 #pragma unroll
@@ -1853,6 +1862,12 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
       if constexpr (FB) ko = (int)((unsigned)ko + kKfHi * (unsigned)PB);  // the unbiased offset
       const int k = live ? a * kBWin - ko / PB + bin - kbias : -1;
       const int t = t0 + a;
+      if constexpr (WBUF) {
+        const int ray = (pl ? 2 * n_ang - 1 - t : t) * n_det + k;
+        const int voff = (live && k >= 0 && k < n_det) ? ray * (VBR * (int)sizeof(T)) : -1;
+        vload<T, PV>(rs_sino, voff, 0, wst[e].v);
+        continue;
+      }
       const size_t ray0 = (size_t)t * n_det + k, ray1 = (size_t)(2 * n_ang - 1 - t) * n_det + k;
       if (live && k >= 0 && k < n_det) {
         if constexpr (NPL == 2) {  // virtual plane pl = orientation pl: one 16-B real plane
