@@ -80,19 +80,19 @@ def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
                        max_iters=10, eps_pri=1e-1, eps_dual=1e-1, phantom_true=None,
                        mu=None, tv_iters=10, cg_iters=5, tv_kind="iso",
                        dtype=np.float64, node_subset=None, fusion="midpoint", Wi_list=None,
-                       inner_tol=None, max_inner_updates=10, node_map=None):
+                       inner_tol=None, max_inner_updates=10, pool=None):
     """Oracle ADMM.  ``ops`` = list of scipy sparse matrices (one per node).
 
     Returns (x_list, history) with the reference's history keys.  With
     ``node_subset`` only those nodes' x-updates run (the others keep x=0); used
     only to time a bounded CPU sample.  ``fusion="weighted"`` needs ``Wi_list``.
-    ``node_map(tasks)`` (fixed-count mode only) runs the iteration's independent node
-    updates -- a list of (i, b_i, D, c, qv, state, N, params, dtype) -- and returns
-    [(state, diag)] in order (oracle/parallel.py: one process per node, Jacobi order,
-    so results equal the sequential loop).
+    ``pool`` (fixed-count mode only; oracle/parallel.NodePool) runs the iteration's
+    independent node updates in worker processes that hold each node's state for the whole
+    trajectory: ``pool.bind(b, params, N, dtype)`` once, then ``pool.update([(i, qv)])`` ->
+    [(x_i, diag)] per iteration (Jacobi order, so results equal the sequential loop).
     """
-    if node_map is not None and inner_tol is not None:
-        raise ValueError("node_map runs fixed-count updates only")
+    if pool is not None and inner_tol is not None:
+        raise ValueError("pool runs fixed-count updates only")
     if fusion not in ("midpoint", "weighted"):
         raise ValueError("fusion must be 'midpoint' or 'weighted'")
     weighted = fusion == "weighted"
@@ -110,8 +110,11 @@ def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
     # scipy matrices; any object with @ and .T (e.g. the GPU RayTransform, used by the
     # full-size tests as an operator-level oracle: this loop's float64 vector algebra
     # around a projector that is itself checked against joseph_matrix)
-    ATs = [A.T.tocsr() if hasattr(A.T, "tocsr") else A.T for A in ops]
-    Atb = [ATs[i] @ b[i] for i in range(V)]
+    if pool is None:
+        ATs = [A.T.tocsr() if hasattr(A.T, "tocsr") else A.T for A in ops]
+        Atb = [ATs[i] @ b[i] for i in range(V)]
+    else:
+        pool.bind(b, prm, N, dtype)
     states = [ns.NodeState.zeros(n, dtype) for _ in range(V)]
     y = {e: np.zeros(n) for e in edges}
     z = {e: np.zeros(n) for e in edges}
@@ -137,19 +140,14 @@ def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
         tasks = []
         for i in todo:
             qv = []
-            D = np.zeros(n)
-            c = np.zeros(n)
             for j in nbrs[i]:
                 e = (min(i, j), max(i, j))
                 yi = y[e] if i == e[0] else (y2[e] if weighted else -y[e])
-                v = z[e] - yi
-                q = np.asarray(Qij_diag_fn(i, j), dtype=np.float64)
-                D += q
-                c += q * v
-                qv.append((q, v))
-            if node_map is not None:
-                tasks.append((i, b[i], D, c, qv, states[i], N, prm, dtype))
+                qv.append((np.asarray(Qij_diag_fn(i, j), dtype=np.float64), z[e] - yi))
+            if pool is not None:
+                tasks.append((i, qv))
                 continue
+            D, c = ns.assemble(qv, n)
             d = ns.node_update(ops[i], Atb[i], b[i], D, c, qv, states[i], N, prm, dtype=dtype,
                                AT=ATs[i])
             nu_i[i] = 1
@@ -169,9 +167,9 @@ def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
             sb_i[i] = d.sb_res
             g_i[i] = d.g_norm
             mse_i[i] = d.mse_sino
-        if node_map is not None:
-            for (i, *_), (st, d) in zip(tasks, node_map(tasks)):
-                states[i] = st
+        if pool is not None:
+            for (i, _), (xi, d) in zip(tasks, pool.update(tasks)):
+                states[i].x = xi
                 nu_i[i] = 1
                 obj_i[i], sb_i[i], g_i[i], mse_i[i] = d.obj, d.sb_res, d.g_norm, d.mse_sino
         x = [st.x.astype(np.float64) for st in states]

@@ -67,6 +67,16 @@ class NodeDiag:
     cg_rr: list = field(default_factory=list)
 
 
+def assemble(qv_terms, n: int):
+    """D = sum_j q_ij, c = sum_j q_ij * v_ij in neighbour order (block_6_admm_loop_ver2.py:137-146)."""
+    D = np.zeros(n)
+    c = np.zeros(n)
+    for q, v in qv_terms:
+        D += q
+        c += q * v
+    return D, c
+
+
 def _dot(a, b) -> float:
     return float(np.dot(a.astype(np.float64), b.astype(np.float64)))
 

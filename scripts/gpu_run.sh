@@ -42,7 +42,7 @@ for step in "$@"; do
       expr=${step#tests=}
       if [ "$expr" = all ]; then k=(); else k=(-k "$expr"); fi
       # -s: tests that run minutes (the 20-iteration C3 oracle) print progress lines to the log
-      run pytest 1100 python -u -m pytest tests -m gpu "${k[@]}" -v -s -rf --timeout 900 --timeout-method thread --durations=15 > gpurun_out/pytest_${TAG}.log 2>&1
+      run pytest 700 python -u -m pytest tests -m gpu "${k[@]}" -v -s -rf --timeout 600 --timeout-method thread --durations=15 > gpurun_out/pytest_${TAG}.log 2>&1
       rc=$?; tail -25 gpurun_out/pytest_${TAG}.log; [ $rc -ne 0 ] && exit $rc ;;
     etests=*)  # etests=VAR=VAL:EXPR -- pytest -m gpu -k EXPR with VAR=VAL in the environment (A/B of a kernel switch)
       v=${step#etests=}; kv=${v%%:*}; expr=${v#*:}

@@ -95,10 +95,12 @@ def test_bench_as_rank_share(cuda):
     assert sh["exchange"]["bytes_received"] == sh["halo_rows"] * 1024 * 1024 * 8
 
 
+@pytest.mark.long
 @pytest.mark.timeout(600)
 def test_bench_default_proxies(cuda):
     """The default one-GPU line's per-rank proxies: C3 on 2 ranks, C4 on 2 / 4 / 8 ranks, each
-    with its measured one-GPU time, the share's time and the predicted speedup."""
+    with its measured one-GPU time, the share's time and the predicted speedup.  (ADMM_TEST_LONG:
+    the driver's own default bench run produces this line every round.)"""
     b = _run("--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--strong-steps", "1", "--proxy-steps", "1")
     px = b["proxy_8gpu"]
     assert set(k for k in px if "@" in k) == {"C3@2", "C4@2", "C4@4", "C4@8"}

@@ -160,9 +160,7 @@ def test_c4_full_graph_matches_operator_oracle(cuda):
     print(f"C4 graph: {G.number_of_edges()} edges, mean degree {2 * G.number_of_edges() / 32:.2f}")
     chk = r1["chk"]
     assert chk["batches"] == 1 and chk["stored_edges"] == G.number_of_edges()
-    assert chk["worst"] < 1e-12, chk
-    r2 = _run("C4")  # bitwise repeatable
-    _same(r1, r2)
+    assert chk["worst"] < 1e-12, chk  # (bitwise repeatability: test_c4_ranks_match_one_rank_bitwise)
     import threading
     stop = threading.Event()
 
@@ -187,10 +185,12 @@ def test_c4_full_graph_matches_operator_oracle(cuda):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("world", [4, 8])
+@pytest.mark.parametrize("world", [pytest.param(4, marks=pytest.mark.long), 8])
 def test_c4_ranks_match_one_rank_bitwise(cuda, world):
-    """C4 sharded over 4 and over 8 ranks (its 8-GPU layout: 4 nodes per rank, node
-    interleave 4, p2p halo exchange chosen on every rank) bitwise equal to one process."""
+    """C4 sharded over 8 ranks (its 8-GPU layout: 4 nodes per rank, node interleave 4, p2p
+    halo exchange chosen on every rank) bitwise equal to one process; 4 ranks with
+    ADMM_TEST_LONG=1.  The one-process run is a fresh process, so this is also C4's
+    run-to-run bitwise repeatability."""
     r1 = _spawn("C4", 1, 500)[0]
     res = _spawn("C4", world, 700)
     for r in range(world):

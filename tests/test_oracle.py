@@ -194,6 +194,27 @@ def test_admm_golden_trajectory():
     assert set(h) == set(oadmm.HISTORY_KEYS) | set(oadmm.EXTRA_KEYS)
 
 
+def test_node_pool_equals_sequential_loop():
+    """oracle/parallel.NodePool (nodes pinned to 2 workers, memory-mapped CSR) gives the
+    sequential loop's trajectory bitwise -- the harness of the C2/C3 GPU trajectory tests."""
+    from oracle.parallel import NodePool
+    N, V = 16, 5
+    A = joseph_matrix(Geometry(N, 12))
+    rng = np.random.default_rng(4)
+    sinos = [A @ shepp_logan(N, 4).reshape(-1) + 0.01 * rng.standard_normal(A.shape[0]) for _ in range(V)]
+    Q = {(i, j): rng.uniform(0.5, 1.5, N * N) for i in range(V) for j in range(V)}
+    kw = dict(lam_tv=0.02, rho=2.0, max_iters=3, eps_pri=0.0, eps_dual=0.0, phantom_true=shepp_logan(N, 4),
+              tv_iters=3, cg_iters=2)
+    G = nx.cycle_graph(V)
+    G.add_edge(0, 2)
+    x1, h1 = oadmm.decentralized_admm([A] * V, sinos, G, lambda i, j: Q[i, j], N, **kw)
+    with NodePool(N, 12, procs=2) as pool:
+        x2, h2 = oadmm.decentralized_admm([pool.A] * V, sinos, G, lambda i, j: Q[i, j], N, pool=pool, **kw)
+    assert np.array_equal(np.stack(x1), np.stack(x2))
+    for k in h1:
+        assert np.array_equal(np.asarray(h1[k]), np.asarray(h2[k]), equal_nan=True), k
+
+
 def test_single_y_form_equals_reference_two_dual_form():
     """The device's single-y edge state reproduces _ver2:210-230 literally."""
     rng = np.random.default_rng(9)
