@@ -98,6 +98,7 @@ class NodeBatch:
                 inc_qslot.append(slots[key])
         self.q = torch.stack(qvecs) if qvecs else torch.zeros((1, n), dtype=torch.float64, device=dev)
         self.n_qslots = len(qvecs)
+        self.inc_qslot_host = list(inc_qslot)
         ii = lambda a: torch.tensor(a if len(a) else [0], dtype=torch.int32, device=dev)  # noqa: E731
         self.inc_off = ii(plan.inc_off)
         self.inc_edge = ii(plan.inc_edge)
@@ -152,6 +153,22 @@ class NodeBatch:
         _lib.check(self.lib.admm_batch_bind(self.ctx.h, C.byref(self.cb)), "admm_batch_bind")
         _lib.check(self.lib.admm_batch_atb(self.ctx.h, p(self.atb), C.c_void_p(self._s())),
                    "admm_batch_atb")
+
+    def set_precisions(self, qs) -> None:
+        """New q_ij for a batch bound with one q slot per incidence (in incidence order): the
+        slots are rewritten, D = sum_j q_ij is recomputed as at construction (same order) and the
+        batch re-bound (its interleaved D samples and recorded sequences are bind-time data).
+        Used by the block_5 drop-in's batch cache."""
+        if len(qs) != len(self.inc_qslot_host) or sorted(self.inc_qslot_host) != list(range(len(qs))):
+            raise ValueError("set_precisions needs one q slot per incidence")
+        for s, q in enumerate(qs):
+            self.q[self.inc_qslot_host[s]].copy_(_as_f64_tensor(q, self.geom.n, self.dev))
+        self.dsum.zero_()
+        for k in range(self.V):
+            for s in range(self.plan.inc_off[k], self.plan.inc_off[k + 1]):
+                self.dsum[k] += self.q[self.inc_qslot_host[s]]
+        torch.cuda.synchronize(self.dev)
+        _lib.check(self.lib.admm_batch_bind(self.ctx.h, C.byref(self.cb)), "admm_batch_bind")
 
     def z_of(self, k: int) -> torch.Tensor:
         """z of stored edge slot k: the stored vector, or (derived) the midpoint of its endpoint

@@ -1272,6 +1272,58 @@ __device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j
       if (u < nv) A.out_d[(size_t)(v0 + u) * npix + pix] = (double)acc[u];
   } else if constexpr (MODE == BACK_WSQ) {
     A.out_d[pix] = fmax((double)acc[0], 1e-12);
+  } else if constexpr (MODE == BACK_H && std::is_same<T, float>::value && VB % 2 == 0) {
+    // float32 samples: H p = acc + rho D p + mu K^T K p formed in float32, two lanes per
+    // packed instruction (p, D and the taps' acc are float32 samples and Hp is stored as one,
+    // so float64 here only re-rounded the same sum), and the five CG dots accumulated in
+    // float64 by explicit fma (p.Hp and Hp.Hp are exact float64 products of float32 values)
+    using F2 = float2v;
+    const T* pv = A.pin + sbase;
+    T pc[VB], pn[VB], dv[VB], outv[VB];
+    F2 kt[VB / 2], pc2[VB / 2];
+    gload<T, VB>(pv + (size_t)pix * VS, pc);
+#pragma unroll
+    for (int h = 0; h < VB / 2; ++h) {
+      pc2[h] = F2{pc[2 * h], pc[2 * h + 1]};
+      kt[h] = F2{0.0f, 0.0f};
+    }
+    // K^T K p in the order of the float64 form: (pc - p_up) - (p_down - pc) + (pc - p_left) - (p_right - pc)
+    auto nb = [&](size_t o, bool sub_pc_first) {
+      gload<T, VB>(pv + o * VS, pn);
+#pragma unroll
+      for (int h = 0; h < VB / 2; ++h) {
+        const F2 q = F2{pn[2 * h], pn[2 * h + 1]};
+        kt[h] = sub_pc_first ? kt[h] + (pc2[h] - q) : kt[h] - (q - pc2[h]);
+      }
+    };
+    if (i >= 1) nb((size_t)(pix - N), true);
+    if (i <= N - 2) nb((size_t)(pix + N), false);
+    if (j >= 1) nb((size_t)(pix - 1), true);
+    if (j <= N - 2) nb((size_t)(pix + 1), false);
+    gload<T, VB>(A.dsum_s + sbase + (size_t)pix * VS, dv);
+    const F2 rho2 = F2{(float)A.rho, (float)A.rho}, mu2 = F2{(float)A.mu, (float)A.mu};
+#pragma unroll
+    for (int h = 0; h < VB / 2; ++h) {
+      const F2 d2 = F2{dv[2 * h], dv[2 * h + 1]} * rho2;
+      F2 hv = __builtin_elementwise_fma(d2, pc2[h], F2{acc[2 * h], acc[2 * h + 1]});
+      hv = __builtin_elementwise_fma(mu2, kt[h], hv);
+      outv[2 * h] = hv.x;
+      outv[2 * h + 1] = hv.y;
+    }
+#pragma unroll
+    for (int u = 0; u < VB; ++u) {
+      if (u >= nv) outv[u] = T(0);
+      if (u < nv) {
+        const double hd = (double)outv[u], pcd = (double)pc[u];
+        const double rv = A.r[(size_t)(v0 + u) * npix + pix];
+        pq[u][0] = fma(pcd, hd, ACC ? pq[u][0] : 0.0);
+        pq[u][1] = fma(rv, hd, ACC ? pq[u][1] : 0.0);
+        pq[u][2] = fma(hd, hd, ACC ? pq[u][2] : 0.0);
+        pq[u][3] = fma(rv, rv, ACC ? pq[u][3] : 0.0);
+        pq[u][4] = fma(rv, pcd, ACC ? pq[u][4] : 0.0);
+      }
+    }
+    gstore<T, VB>(A.out_t + sbase + (size_t)pix * VS, outv);
   } else if constexpr (MODE == BACK_H || MODE == BACK_INIT) {
     // H v = acc + rho D v + mu K^T K v  (v = p or xs, interleaved samples)
     const T* pv = A.pin + sbase;

@@ -221,6 +221,77 @@ def test_build_node_problem_matches_oracle(cuda):
     assert prob.solver_stats.num_iters == 50 and prob.status == "optimal_inaccurate"
 
 
+def test_build_node_problem_cached_in_ver2_loop(cuda):
+    """The reference's own loop shape (block_6_admm_loop_ver2.py:81-123, 210-230): a new
+    build_node_problem per node per outer iteration, the literal _ver2 edge updates between the
+    iterations (oracle.admm.edge_update_literal).  4-node ring at 512^2 (C3's image), 5 outer
+    iterations = 20 calls.  The cached batches with warm_start=False give bitwise the uncached
+    path; warm_start=True (the reference's keyword) continues each node from its previous
+    x-update; a cached call costs at most 2x the x-update it replays."""
+    import time
+    import block_5_node_problem as b5
+    N, V, iters = 512, 4, 5
+    ops = make_operators(N, V, 96 * V, dtype="float32", device=0)
+    sinos = [s.reshape(-1) for s in make_sinograms(ops, shepp_logan(N), 0.005, seed=1000)]
+    Wi, Q = make_precisions(ops)
+    G = nx.cycle_graph(V)
+
+    def loop(cache, warm):
+        b5.clear_cache()
+        b5.CACHE_ENTRIES = 256 if cache else 0
+        x = [np.zeros(N * N) for _ in range(V)]
+        y = {(min(i, j), max(i, j), k): np.zeros(N * N) for i, j in G.edges() for k in (i, j)}
+        z = {(min(i, j), max(i, j)): np.zeros(N * N) for i, j in G.edges()}
+        out, t_call, t_upd = [], [], []
+        for _ in range(iters):
+            new_x = [None] * V
+            for i in range(V):
+                vs, qs = [], []
+                for j in G.neighbors(i):
+                    key = (min(i, j), max(i, j))
+                    vs.append(z[key] - y[(key[0], key[1], i)])
+                    qs.append(Q(i, j))
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                xi, prob = b5.build_node_problem(ops[i], sinos[i], 2.0, vs, N, 0.02, qs)
+                prob.solve(solver="SCS", eps=1e-2, max_iters=50, acceleration_lookback=20, verbose=False,
+                           warm_start=warm)
+                t_call.append(time.perf_counter() - t0)
+                new_x[i] = xi.value
+                out.append((xi.value.copy(), prob.value))
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                if cache:  # the x-update alone, replayed once more on a scratch copy of the state
+                    nb = prob.nb
+                    saved = [t.clone() for t in (nb.x_ext, nb.d, nb.e)]
+                    ev[0].record()
+                    nb.node_update()
+                    ev[1].record()
+                    torch.cuda.synchronize()
+                    t_upd.append(ev[0].elapsed_time(ev[1]) * 1e-3)
+                    for t, s in zip((nb.x_ext, nb.d, nb.e), saved):
+                        t.copy_(s)
+            x = new_x
+            z, y = oadmm.edge_update_literal(G, x, y, z)
+        return out, t_call, t_upd
+
+    try:
+        ref, t_fresh, _ = loop(False, False)
+        cold, t_cold, _ = loop(True, False)
+        for (xa, va), (xb, vb) in zip(ref, cold):
+            assert np.array_equal(xa, xb) and va == vb
+        warm, t_warm, t_upd = loop(True, True)
+    finally:
+        b5.clear_cache()
+        b5.CACHE_ENTRIES = 256
+    # warm starts: the first iteration's calls are the cold ones; later ones move less
+    assert all(np.array_equal(a[0], b[0]) for a, b in zip(ref[:V], warm[:V]))
+    call = float(np.median(t_warm[V:]))
+    upd = float(np.median(t_upd[V:]))
+    print(f"per call: uncached {np.median(t_fresh[V:]) * 1e3:.2f} ms, cached cold {np.median(t_cold[V:]) * 1e3:.2f} ms, "
+          f"cached warm {call * 1e3:.2f} ms; one replayed x-update {upd * 1e3:.2f} ms")
+    assert call <= 2.0 * upd, (call, upd)
+
+
 def test_build_node_problem_no_neighbours_no_tv(cuda):
     """test_block5_with_aggregate.py:59-67 shape: rho=0, no neighbours; lam=0 -> least squares."""
     N = 24
