@@ -240,7 +240,7 @@ def cpu_baseline(N, a, b, q, x_gpu, procs=None, budget=CPU_BASELINE_SECONDS):
 # MI355X_MICROARCH.md gfx950 correction), one per headline workload: the per-launch
 # figure depends on the node chunks one launch projects.  PMC counters cannot be read
 # inside this run.
-TRAFFIC_FILES = {"C3": "profiles/r5_traffic.json", "weak8": "profiles/r5_traffic_weak8.json"}
+TRAFFIC_FILES = {"C3": "profiles/r6_traffic.json", "weak8": "profiles/r6_traffic_weak8.json"}
 
 
 def fwd_kernel_traffic(tr, tname, vb, mirror):
@@ -253,15 +253,43 @@ def fwd_kernel_traffic(tr, tname, vb, mirror):
     return tr["kernels"].get(want, {}).get("hbm_bytes_per_launch")
 
 
+KERNEL_SOURCES = ("distributed-inverse-problem-admm_amd/csrc/kernels.hpp",
+                  "distributed-inverse-problem-admm_amd/csrc/admm_tomo.hip")
+
+
+def kernel_source_sha16():
+    """sha256 (first 16 hex digits) of the kernel sources the library is built from; a PMC
+    traffic file records the hash of the sources it measured (scripts/traffic_summary.py)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+TRAFFIC_STALE = {}  # workload -> why its traffic file was not used
+
+
 def pmc_traffic(workload):
+    """The committed PMC traffic of ``workload`` -- only if it was measured on kernels built
+    from the current sources (same kernel_source_sha16); otherwise (None, file) and the reason
+    in TRAFFIC_STALE: the line then carries traffic null rather than bytes of older kernels."""
     f = TRAFFIC_FILES.get(workload)
     if f is None:
         return None, None
     try:
         with open(os.path.join(ROOT, f)) as fh:
-            return json.load(fh), f
+            tr = json.load(fh)
     except (OSError, ValueError):
+        TRAFFIC_STALE[workload] = f"{f}: missing or unreadable"
         return None, f
+    want, have = kernel_source_sha16(), tr.get("kernel_source_sha16")
+    if have != want:
+        TRAFFIC_STALE[workload] = (f"{f} measured kernels of source hash {have}, the library is built from "
+                                   f"{want}: traffic not reused")
+        return None, f
+    return tr, f
 
 
 STREAMS = 1  # concurrent batch streams per rank (--streams; RankGroups)
@@ -440,6 +468,25 @@ def proxy(name, world, t1_ms, V_total, steps, warmup):
             "predicted_speedup_one_link": t1_ms / t_1, "predicted_speedup_direct": t1_ms / t_d}
 
 
+def proxy_weak(world, value_1, steps, warmup):
+    """proxy_8gpu entry of the N-GPU headline (weak scaling: ``weak8``, a ring of 8 x world
+    nodes, 8 per rank): the busiest rank's share timed here plus its exchange; the predicted
+    whole-job value (node-updates/s) and its ratio to the one-GPU headline ``value_1`` (C3 on
+    this GPU) -- the ratio the driver's scaling run computes from its own per-N lines."""
+    ranks = sorted({0, busiest_rank("weak8", world)})
+    shares = [time_share("weak8", world, r, steps, warmup) for r in ranks]
+    worst = max(shares, key=lambda s: s["ms_per_step"] + s["exchange"]["ms_conservative"])
+    V_total = workload_cfg("weak8", world)["nodes"]
+    out = {"config": "weak8", "ranks": world, "nodes": V_total, "shares": shares,
+           "one_gpu_value": value_1, "scaling": "weak"}
+    for tag, key in (("", "ms_conservative"), ("_one_link", "ms_one_link"), ("_direct", "ms_direct")):
+        t = worst["ms_per_step"] + worst["exchange"][key]
+        out[f"predicted_value{tag}"] = V_total * 1e3 / t
+        out[f"predicted_speedup{tag}"] = V_total * 1e3 / t / value_1
+    out["predicted_ms_per_step"] = worst["ms_per_step"] + worst["exchange"]["ms_conservative"]
+    return out
+
+
 def launch_ranks(n: int) -> int:
     """Run this script as ``n`` rank processes (one per GPU) and return the exit status.
 
@@ -485,21 +532,25 @@ def back_kernel_traffic(tr, tname, vb, mirror):
     return tr["kernels"].get(want, {}).get("hbm_bytes_per_launch")
 
 
-def _roof(kernel, traffic, tr_file, ms, compulsory, lds_bytes, extra=None):
+def _roof(kernel, traffic, tr_file, ms, compulsory, lds_bytes, extra=None, stale=None):
     """One kernel's roofline entry: PMC bytes per launch / live event-timed in-solve duration
     against the 8 TB/s HBM peak, compulsory bytes beside it, LDS tap reads against the
-    aggregate ds_read_b128 rate."""
+    aggregate ds_read_b128 rate.  Without a PMC file of the current kernel sources (``stale``
+    says why) ``traffic`` is null and ``achieved`` falls back to the compulsory bytes."""
     s = ms * 1e-3
+    basis = traffic if traffic is not None else compulsory
     roof = {
         "kernel": kernel,
         "bound": "hbm",
-        "achieved": traffic / s / 1e9 if traffic is not None else None,
+        "achieved": basis / s / 1e9,
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
-        "frac": traffic / s / 1e9 / HBM_PEAK_GBS if traffic is not None else None,
+        "frac": basis / s / 1e9 / HBM_PEAK_GBS,
         "traffic": traffic,
+        "achieved_basis": "pmc" if traffic is not None else "compulsory",
         "traffic_source": (f"{tr_file}: rocprofv3 PMC 2 x FETCH_SIZE + WRITE_SIZE per in-solve launch "
-                           "(Infinity-Cache hits included)") if traffic is not None else None,
+                           "(Infinity-Cache hits included), measured on kernels of source hash "
+                           f"{kernel_source_sha16()}") if traffic is not None else stale,
         "avg_launch_ms": ms,
         "compulsory_bytes": compulsory,
         "compulsory_frac": compulsory / s / 1e9 / HBM_PEAK_GBS,
@@ -516,8 +567,7 @@ def _roof(kernel, traffic, tr_file, ms, compulsory, lds_bytes, extra=None):
         },
     }
     roof.update(extra or {})
-    if roof["frac"] is not None:
-        assert roof["frac"] <= 1.0, roof
+    assert roof["frac"] <= 1.0, roof
     return roof
 
 
@@ -541,6 +591,7 @@ def projector_rooflines(r, workload, fwd_reps):
     V, vb, mirror = nb.V, nb.ctx_vb, nb.mirror
     n, m = n_img * n_img, a_node * n_img
     tr, tr_file = pmc_traffic(workload)
+    stale = TRAFFIC_STALE.get(workload)
     tname = "double" if dtype == "float64" else "float"
     vbv = min(2 * vb, 32 // sb)  # mirror mode's virtual width
     chunks = f"{V} nodes = {-(-V // vb)} node chunk(s) per launch"
@@ -560,7 +611,7 @@ def projector_rooflines(r, workload, fwd_reps):
                          "(HIP events around each CG-step forward of one x-update) / 8 TB/s. compulsory = "
                          "each node image read once + its sinogram written once. sample_touch (SURVEY 8d) "
                          "counts every tap as a load; taps are LDS reads, so it is a reuse factor, not an "
-                         "HBM rate (see DESIGN.md)"})
+                         "HBM rate (see DESIGN.md)"}, stale)
     # back projector in H mode (A^T s fused with H p = A^T A p + rho D p + mu K^T K p and the five
     # CG dot products): compulsory = sinogram, p, D (samples) and r (float64) read once, Hp written
     back_comp = V * m * sb + 3 * V * n * sb + V * n * 8
@@ -574,7 +625,7 @@ def projector_rooflines(r, workload, fwd_reps):
                   "note": "frac = PMC bytes per launch / live event-timed duration of the in-solve launches "
                           "(HIP events around each CG-step back projection of one x-update) / 8 TB/s. "
                           "compulsory = sinogram, p, D read once as samples, r (float64) read once, Hp "
-                          "written once"})
+                          "written once"}, stale)
     dom = dict(back if back_ms >= fwd_ms else fwd)
     dom["dominant_by"] = (f"in-solve time per CG step: back {back_ms * 1e3:.1f} us vs forward taps "
                           f"{fwd_ms * 1e3:.1f} us (one launch each per CG step)")
@@ -628,9 +679,10 @@ def main():
                     help="strong-scaling configs measured after the headline, comma separated "
                          "(default: C4 on one GPU, C3,C4 on N > 1; 'none' to skip)")
     ap.add_argument("--strong-steps", type=int, default=5)
-    ap.add_argument("--proxy", choices=("none", "fast", "all"), default="fast",
+    ap.add_argument("--proxy", choices=("none", "fast", "all"), default="all",
                     help="one GPU only: per-rank proxies of the multi-GPU runs (fast: C3 on 2, C4 on 2/4/8 "
-                         "ranks; all: + C5 on 8 ranks, which also times C5 on one GPU)")
+                         "ranks; all (default): + C5 on 8 ranks, which also times C5 on one GPU, and the "
+                         "weak-scaling headline on 8 ranks)")
     ap.add_argument("--proxy-steps", type=int, default=6)
     ap.add_argument("--streams", type=int, default=STREAMS,
                     help="split each rank's nodes into up to this many batches (>= 8 float32 / 4 float64 "
@@ -772,13 +824,17 @@ def main():
                 t1[name] = (s["nodes"], s["ms_per_step"])
             V, t = t1[name]
             px[f"{name}@{W}"] = proxy(name, W, t, V, args.proxy_steps, 1)
+        if args.proxy == "all" and workload == "C3":
+            px["weak8@8"] = proxy_weak(8, value, args.proxy_steps, 1)
         result["proxy_8gpu"] = dict(
             px, model=f"T_rank = rank's share timed on this GPU (halo rows fixed); exchange = bytes received "
                       f"(float64 images + statistics) over xGMI at {XGMI_LINK_GBS:.0f} GB/s per link: "
                       f"conservative = one link + {RCCL_CALL_US:.0f} us per RCCL call (assumed; 2 calls per "
                       f"iteration), one_link = one link, direct = min(peers, {XGMI_LINKS}) links; "
-                      f"predicted_speedup = T_1 / (T_rank + exchange_conservative); only the rank-internal "
-                      f"edge updates overlap the all-gather (not priced)")
+                      f"predicted_speedup = T_1 / (T_rank + exchange_conservative); weak8@8: predicted_value = 64 "
+                      f"nodes / (T_rank + exchange), predicted_speedup = predicted_value / the one-GPU headline "
+                      f"value; the rank-internal edge updates overlap the halo exchange (p2p or all-gather; "
+                      f"not priced)")
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

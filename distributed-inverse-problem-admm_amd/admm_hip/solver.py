@@ -239,8 +239,12 @@ class NodeBatch:
     def consensus_range(self, e0: int, e1: int, rows: int) -> None:
         """Edge updates of stored slots [e0, e1) only, whose endpoints lie in x_ext rows [0, rows)
         (stored z, midpoint fusion; admm_consensus_range, ABI 9): the same per-edge results and
-        statistics as ``consensus``."""
+        statistics as ``consensus``.  The endpoint rows are checked here against ``rows`` (the
+        library reads only rows below it while the halo rows may still be landing)."""
         if e1 > e0:
+            top = max(max(self.plan.edge_a_row[e0:e1]), max(self.plan.edge_b_row[e0:e1]))
+            if top >= rows:
+                raise ValueError(f"edge slots [{e0}, {e1}) reach x_ext row {top} >= rows={rows}")
             _lib.check(self.lib.admm_consensus_range(self.ctx.h, int(e0), int(e1), int(rows), C.c_void_p(self._s())),
                        "admm_consensus_range")
 

@@ -955,6 +955,15 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
     const double kmn = C->Kb - c0 * (std::fabs(ba[t].Bi) + std::fabs(ba[t].Bj));
     C->kbias = std::max(C->kbias, (int)std::ceil(-kmn) + 2);
   }
+  // the float taps' kf_split needs k_f + kbias in (0, 2^20) for every pixel and angle (the sum
+  // with 2^20 must stay in [2^20, 2^21)); a detector far off the image could break that
+  for (int t = 0; t < g.n_angles; ++t) {
+    const double kmx = C->Kb + C->kbias + c0 * (std::fabs(ba[t].Bi) + std::fabs(ba[t].Bj)) + 2.0;
+    if (kmx >= 1048576.0) {
+      delete C;  // (nothing allocated on the device yet)
+      return fail(ADMM_E_INVALID, "detector offset puts a bin position past 2^20 (kf_split)");
+    }
+  }
   // exact power-of-two scalings: 2^-wexp (N < 3: L = 2 / (N |cos|) can exceed 1) on ws and wc, and
   // 2^-32 on ws, whose float taps multiply frac(k_f) x 2^32 (kernels.hpp kf_split)
   for (int t = 0; t < g.n_angles; ++t) {

@@ -1272,44 +1272,51 @@ __device__ __forceinline__ void back_epilogue(const BackArgs<T>& A, int i, int j
       if (u < nv) A.out_d[(size_t)(v0 + u) * npix + pix] = (double)acc[u];
   } else if constexpr (MODE == BACK_WSQ) {
     A.out_d[pix] = fmax((double)acc[0], 1e-12);
-  } else if constexpr (MODE == BACK_H && std::is_same<T, float>::value && VB % 2 == 0) {
-    // float32 samples: H p = acc + rho D p + mu K^T K p formed in float32, two lanes per
-    // packed instruction (p, D and the taps' acc are float32 samples and Hp is stored as one,
-    // so float64 here only re-rounded the same sum), and the five CG dots accumulated in
-    // float64 by explicit fma (p.Hp and Hp.Hp are exact float64 products of float32 values)
+  } else if constexpr (MODE == BACK_H && std::is_same<T, float>::value) {
+    // float32 samples: H p = acc + rho D p + mu K^T K p formed in float32 (p, D and the taps'
+    // acc are float32 samples and Hp is stored as one, so float64 here only re-rounded the same
+    // sum), lane pairs as packed instructions -- every lane the same IEEE single ops whether it
+    // is packed or the odd tail, so a node's result does not depend on the batch width -- and
+    // the five CG dots accumulated in float64 by explicit fma (p.Hp and Hp.Hp are exact float64
+    // products of float32 values)
     using F2 = float2v;
+    constexpr int NP = VB / 2;
     const T* pv = A.pin + sbase;
     T pc[VB], pn[VB], dv[VB], outv[VB];
-    F2 kt[VB / 2], pc2[VB / 2];
+    F2 kt2[NP > 0 ? NP : 1], pc2[NP > 0 ? NP : 1];
+    float kt1 = 0.0f;  // (odd VB: the last lane)
     gload<T, VB>(pv + (size_t)pix * VS, pc);
 #pragma unroll
-    for (int h = 0; h < VB / 2; ++h) {
+    for (int h = 0; h < NP; ++h) {
       pc2[h] = F2{pc[2 * h], pc[2 * h + 1]};
-      kt[h] = F2{0.0f, 0.0f};
+      kt2[h] = F2{0.0f, 0.0f};
     }
     // K^T K p in the order of the float64 form: (pc - p_up) - (p_down - pc) + (pc - p_left) - (p_right - pc)
     auto nb = [&](size_t o, bool sub_pc_first) {
       gload<T, VB>(pv + o * VS, pn);
 #pragma unroll
-      for (int h = 0; h < VB / 2; ++h) {
+      for (int h = 0; h < NP; ++h) {
         const F2 q = F2{pn[2 * h], pn[2 * h + 1]};
-        kt[h] = sub_pc_first ? kt[h] + (pc2[h] - q) : kt[h] - (q - pc2[h]);
+        kt2[h] = sub_pc_first ? kt2[h] + (pc2[h] - q) : kt2[h] - (q - pc2[h]);
       }
+      if constexpr (VB % 2) kt1 = sub_pc_first ? kt1 + (pc[VB - 1] - pn[VB - 1]) : kt1 - (pn[VB - 1] - pc[VB - 1]);
     };
     if (i >= 1) nb((size_t)(pix - N), true);
     if (i <= N - 2) nb((size_t)(pix + N), false);
     if (j >= 1) nb((size_t)(pix - 1), true);
     if (j <= N - 2) nb((size_t)(pix + 1), false);
     gload<T, VB>(A.dsum_s + sbase + (size_t)pix * VS, dv);
-    const F2 rho2 = F2{(float)A.rho, (float)A.rho}, mu2 = F2{(float)A.mu, (float)A.mu};
+    const float rf = (float)A.rho, mf = (float)A.mu;
+    const F2 rho2 = F2{rf, rf}, mu2 = F2{mf, mf};
 #pragma unroll
-    for (int h = 0; h < VB / 2; ++h) {
+    for (int h = 0; h < NP; ++h) {
       const F2 d2 = F2{dv[2 * h], dv[2 * h + 1]} * rho2;
       F2 hv = __builtin_elementwise_fma(d2, pc2[h], F2{acc[2 * h], acc[2 * h + 1]});
-      hv = __builtin_elementwise_fma(mu2, kt[h], hv);
+      hv = __builtin_elementwise_fma(mu2, kt2[h], hv);
       outv[2 * h] = hv.x;
       outv[2 * h + 1] = hv.y;
     }
+    if constexpr (VB % 2) outv[VB - 1] = fmaf(mf, kt1, fmaf(dv[VB - 1] * rf, pc[VB - 1], acc[VB - 1]));
 #pragma unroll
     for (int u = 0; u < VB; ++u) {
       if (u >= nv) outv[u] = T(0);

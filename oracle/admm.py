@@ -29,6 +29,8 @@ z = (W_a a_a + W_b a_b)/(W_a + W_b),  y_e += x_a - z,  y2_e += x_b - z.
 from __future__ import annotations
 
 import math
+import threading
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -76,11 +78,32 @@ def edge_update_literal(G, x, y, z, Wi_list=None):
     return new_z, new_y
 
 
+class _Serialized:
+    """An operator whose products run one at a time (a lock shared by every node's operator
+    and adjoint): the GPU RayTransform of the operator-level oracle shares one context --
+    and its scratch buffers -- per geometry, so concurrent node threads must not interleave
+    its launches.  Only the products serialize; the float64 vector algebra runs in parallel."""
+
+    def __init__(self, op, lock, T=None):
+        self.op, self.lock, self._T = op, lock, T
+        self.shape = op.shape
+
+    @property
+    def T(self):
+        if self._T is None:
+            self._T = _Serialized(self.op.T, self.lock, self)
+        return self._T
+
+    def __matmul__(self, x):
+        with self.lock:
+            return self.op @ x
+
+
 def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
                        max_iters=10, eps_pri=1e-1, eps_dual=1e-1, phantom_true=None,
                        mu=None, tv_iters=10, cg_iters=5, tv_kind="iso",
                        dtype=np.float64, node_subset=None, fusion="midpoint", Wi_list=None,
-                       inner_tol=None, max_inner_updates=10, pool=None):
+                       inner_tol=None, max_inner_updates=10, pool=None, threads=None):
     """Oracle ADMM.  ``ops`` = list of scipy sparse matrices (one per node).
 
     Returns (x_list, history) with the reference's history keys.  With
@@ -90,7 +113,15 @@ def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
     independent node updates in worker processes that hold each node's state for the whole
     trajectory: ``pool.bind(b, params, N, dtype)`` once, then ``pool.update([(i, qv)])`` ->
     [(x_i, diag)] per iteration (Jacobi order, so results equal the sequential loop).
+    ``threads`` (fixed-count mode only; the operator-level oracle over GPU RayTransforms) runs
+    an iteration's node updates in that many threads, the operator products serialized
+    (``_Serialized``): the same per-node arithmetic, so the same results.
     """
+    if threads is not None and (inner_tol is not None or pool is not None):
+        raise ValueError("threads runs fixed-count updates without a pool only")
+    if threads is not None and threads > 1:
+        lock = threading.Lock()
+        ops = [_Serialized(A, lock) for A in ops]
     if pool is not None and inner_tol is not None:
         raise ValueError("pool runs fixed-count updates only")
     if fusion not in ("midpoint", "weighted"):
@@ -144,7 +175,7 @@ def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
                 e = (min(i, j), max(i, j))
                 yi = y[e] if i == e[0] else (y2[e] if weighted else -y[e])
                 qv.append((np.asarray(Qij_diag_fn(i, j), dtype=np.float64), z[e] - yi))
-            if pool is not None:
+            if pool is not None or (threads is not None and threads > 1):
                 tasks.append((i, qv))
                 continue
             D, c = ns.assemble(qv, n)
@@ -167,6 +198,14 @@ def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
             sb_i[i] = d.sb_res
             g_i[i] = d.g_norm
             mse_i[i] = d.mse_sino
+        if threads is not None and threads > 1 and tasks:
+            with ThreadPoolExecutor(threads) as ex:
+                done = list(ex.map(lambda t: ns.node_update(ops[t[0]], Atb[t[0]], b[t[0]], *ns.assemble(t[1], n),
+                                                            t[1], states[t[0]], N, prm, dtype=dtype,
+                                                            AT=ATs[t[0]]), tasks))
+            for (i, _), d in zip(tasks, done):
+                nu_i[i] = 1
+                obj_i[i], sb_i[i], g_i[i], mse_i[i] = d.obj, d.sb_res, d.g_norm, d.mse_sino
         if pool is not None:
             for (i, _), (xi, d) in zip(tasks, pool.update(tasks)):
                 states[i].x = xi

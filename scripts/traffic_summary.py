@@ -15,7 +15,11 @@ import collections
 import csv
 import glob
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import KERNEL_SOURCES, kernel_source_sha16  # noqa: E402  (the hash bench.py checks)
 
 tag, steps, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
 MARK = "k_tv_grad"
@@ -65,6 +69,7 @@ for k, v in acc.items():
 json.dump({"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), tag {tag}, "
                      f"launches between the bench's two marker kernels ({steps} timed steps)",
            "correction": "hbm = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), MI355X_MICROARCH.md HBM",
+           "kernel_source_sha16": kernel_source_sha16(), "kernel_sources": list(KERNEL_SOURCES),
            "per_step": {"hbm_bytes": (2.0 * tot_f + tot_w) / steps, "fetch_size_bytes": tot_f / steps,
                         "write_size_bytes": tot_w / steps, "steps": steps},
            "kernels": res}, open(out, "w"), indent=1, sort_keys=True)

@@ -75,10 +75,11 @@ def test_roofline_traffic_lookup_finds_committed_kernels():
     """bench.py's roofline reads both projectors' PMC bytes per launch from the committed
     traffic files by their full template names (mirror mode at C3: 4-node real vectors,
     8-lane virtual ones)."""
+    import json
     sys.path.insert(0, ROOT)
     import bench
-    tr, f = bench.pmc_traffic("C3")
-    assert tr is not None, f
+    with open(os.path.join(ROOT, bench.TRAFFIC_FILES["C3"])) as fh:
+        tr = json.load(fh)
     back = bench.back_kernel_traffic(tr, "float", 4, True)
     fwd = bench.fwd_kernel_traffic(tr, "float", 4, True)
     assert back is not None and fwd is not None
@@ -87,3 +88,35 @@ def test_roofline_traffic_lookup_finds_committed_kernels():
     V, n, m = 16, 512 * 512, 96 * 512
     assert back > V * m * 4 + 3 * V * n * 4 + V * n * 8
     assert fwd > V * n * 4 + V * m * 4
+
+
+def test_roofline_traffic_bound_to_kernel_sources(tmp_path, monkeypatch):
+    """A PMC traffic file is used only if it records the hash of the kernel sources the
+    library is built from; otherwise the line carries traffic null, the
+    reason, and achieved on the compulsory bytes."""
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    with open(os.path.join(ROOT, bench.TRAFFIC_FILES["C3"])) as fh:
+        tr = json.load(fh)
+    for sha, ok in ((bench.kernel_source_sha16(), True), ("0" * 16, False)):
+        f = tmp_path / f"t_{ok}.json"
+        f.write_text(json.dumps(dict(tr, kernel_source_sha16=sha)))
+        monkeypatch.setitem(bench.TRAFFIC_FILES, "C3", str(f))
+        bench.TRAFFIC_STALE.clear()
+        got, _ = bench.pmc_traffic("C3")
+        assert (got is not None) == ok
+        assert ("C3" in bench.TRAFFIC_STALE) == (not ok)
+    r = bench._roof("k", None, str(f), 0.05, 8e7, 1e9, stale=bench.TRAFFIC_STALE["C3"])
+    assert r["traffic"] is None and r["achieved_basis"] == "compulsory" and "source hash" in r["traffic_source"]
+    assert abs(r["frac"] - 8e7 / 0.05e-3 / 1e9 / bench.HBM_PEAK_GBS) < 1e-12
+
+
+def test_committed_traffic_matches_kernel_sources():
+    """The committed traffic files were measured on the kernels the sources build today."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for wl in ("C3", "weak8"):
+        bench.TRAFFIC_STALE.clear()
+        tr, f = bench.pmc_traffic(wl)
+        assert tr is not None, bench.TRAFFIC_STALE

@@ -30,6 +30,7 @@ from oracle import admm as oadmm
 from oracle.parallel import NodePool
 
 pytestmark = pytest.mark.gpu
+ORACLE_THREADS = 8  # the operator-level oracle's node updates in threads (the box's 16-core share)
 
 
 def rel(a, b):
@@ -146,7 +147,7 @@ def test_large_x_updates_match_operator_oracle(cuda, monkeypatch, N, V, dtype, t
     sin_h = [s.double().cpu().numpy() for s in sinos]
     xo, ho = oadmm.decentralized_admm(ops, sin_h, G, Q, N, lam_tv=0.02, rho=2.0, max_iters=2,
                                       eps_pri=0.0, eps_dual=0.0, phantom_true=ph, tv_kind=tv,
-                                      tv_iters=tvi)
+                                      tv_iters=tvi, threads=ORACLE_THREADS)
     check(x, h, xo, ho, tol)
 
 
@@ -165,7 +166,7 @@ def test_c5_share_full_inner_count_matches_operator_oracle(cuda):
     sin_h = [s.double().cpu().numpy() for s in sinos]
     xo, ho = oadmm.decentralized_admm(ops, sin_h, G, Q, N, lam_tv=0.02, rho=2.0, max_iters=2,
                                       eps_pri=0.0, eps_dual=0.0, phantom_true=ph, tv_kind="aniso",
-                                      tv_iters=10, cg_iters=5)
+                                      tv_iters=10, cg_iters=5, threads=ORACLE_THREADS)
     check(x, h, xo, ho, 1e-9)
     for k in ("obj_per_node", "mse_sino_per_node", "img_mse_per_node", "pri_per_node", "dual_per_node"):
         e = rel(np.stack(h[k]), np.stack(ho[k]))

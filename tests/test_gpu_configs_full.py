@@ -30,6 +30,7 @@ import pytest
 import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
+ORACLE_THREADS = 8  # the operator-level oracle's node updates in threads (the box's 16-core share)
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 
@@ -173,7 +174,8 @@ def test_c4_full_graph_matches_operator_oracle(cuda):
     hb.start()
     try:
         xo, ho = oadmm.decentralized_admm(ops, r1["sinos"], G, Q, c["N"], lam_tv=0.02, rho=2.0,
-                                          max_iters=c["iters"], eps_pri=0.0, eps_dual=0.0, phantom_true=ph)
+                                          max_iters=c["iters"], eps_pri=0.0, eps_dual=0.0, phantom_true=ph,
+                                          threads=ORACLE_THREADS)
     finally:
         stop.set()
     h = r1["hist"]

@@ -195,8 +195,9 @@ def test_admm_golden_trajectory():
 
 
 def test_node_pool_equals_sequential_loop():
-    """oracle/parallel.NodePool (nodes pinned to 2 workers, memory-mapped CSR) gives the
-    sequential loop's trajectory bitwise -- the harness of the C2/C3 GPU trajectory tests."""
+    """oracle/parallel.NodePool (nodes pinned to 2 workers, memory-mapped CSR) and the threaded
+    node updates give the sequential loop's trajectory bitwise -- the harnesses of the C2/C3
+    GPU trajectory tests and of the operator-level (C4/C5-size) ones."""
     from oracle.parallel import NodePool
     N, V = 16, 5
     A = joseph_matrix(Geometry(N, 12))
@@ -210,9 +211,12 @@ def test_node_pool_equals_sequential_loop():
     x1, h1 = oadmm.decentralized_admm([A] * V, sinos, G, lambda i, j: Q[i, j], N, **kw)
     with NodePool(N, 12, procs=2) as pool:
         x2, h2 = oadmm.decentralized_admm([pool.A] * V, sinos, G, lambda i, j: Q[i, j], N, pool=pool, **kw)
-    assert np.array_equal(np.stack(x1), np.stack(x2))
-    for k in h1:
-        assert np.array_equal(np.asarray(h1[k]), np.asarray(h2[k]), equal_nan=True), k
+    # the operator-level oracle's threaded node updates (products serialized)
+    x3, h3 = oadmm.decentralized_admm([A] * V, sinos, G, lambda i, j: Q[i, j], N, threads=3, **kw)
+    for xo, ho in ((x2, h2), (x3, h3)):
+        assert np.array_equal(np.stack(x1), np.stack(xo))
+        for k in h1:
+            assert np.array_equal(np.asarray(h1[k]), np.asarray(ho[k]), equal_nan=True), k
 
 
 def test_single_y_form_equals_reference_two_dual_form():
