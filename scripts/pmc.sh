@@ -12,7 +12,7 @@ i=0
 if [ -n "${PASSFILE:-}" ]; then mapfile -t PASSLIST < "$PASSFILE"; else PASSLIST=("FETCH_SIZE" "WRITE_SIZE"); fi
 for counters in "${PASSLIST[@]}"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $counters --kernel-trace -d gpurun_out/${TAG}_$i -o run --output-format csv -- python bench.py --steps $STEPS --warmup 1 --no-cpu-baseline --headline-only --workload ${WORKLOAD:-C3} > gpurun_out/${TAG}_$i.log 2>&1
+  timeout -s KILL ${PASS_TIMEOUT:-300} rocprofv3 --pmc $counters --kernel-trace -d gpurun_out/${TAG}_$i -o run --output-format csv -- python bench.py --steps $STEPS --warmup 1 --no-cpu-baseline --headline-only --workload ${WORKLOAD:-C3} > gpurun_out/${TAG}_$i.log 2>&1
   rc=$?
   echo "pass $i ($counters) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/${TAG}_$i.log; exit $rc; fi
