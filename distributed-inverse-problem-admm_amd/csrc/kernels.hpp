@@ -2347,6 +2347,9 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // The CG directions whose x steps the fused TV update applies (FUSE): p[k] with alpha_k
 // from the reduction redH + k * 5V, k = 0 .. K-1 (K = 1: only the round's last step).
 constexpr int kMaxCgRing = 8;
+#ifndef ADMM_TV_ALIGN
+#define ADMM_TV_ALIGN 1
+#endif
 template <typename T>
 struct PRing {
   const T* p[kMaxCgRing];
@@ -2395,7 +2398,21 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
     }
     __syncthreads();
     for (int q = threadIdx.x; q < PR * PC; q += kBlock) {
+#if ADMM_TV_ALIGN
+      // the tile's kTile columns first (rows of 256-B-aligned float64 runs per node), the two
+      // halo columns after them: no lane group straddles a cache line
+      int rr, cc;
+      if (q < PR * kTile) {
+        rr = q / kTile;
+        cc = 1 + q % kTile;
+      } else {
+        const int h = q - PR * kTile;
+        rr = h >> 1;
+        cc = (h & 1) ? PC - 1 : 0;
+      }
+#else
       const int rr = q / PC, cc = q % PC;
+#endif
       const int i = i0 - 1 + rr, j = j0 - 1 + cc;
       if (i < 0 || j < 0 || i >= N || j >= N) continue;
       const int o = i * N + j;
@@ -2442,8 +2459,24 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
     // column-fastest: a wave reads runs of 33 consecutive pixels of one node
     __shared__ double qx_s[HR][VB][HC], qy_s[HR][VB][HC];
     for (int q = threadIdx.x; q < HR * HC * VB; q += kBlock) {
+#if ADMM_TV_ALIGN
+      // (as above: the kTile tile columns of every (row, node) first, the halo column after)
+      int cc, u, rr;
+      if (q < HR * VB * kTile) {
+        cc = 1 + q % kTile;
+        const int rest = q / kTile;
+        u = rest % VB;
+        rr = rest / VB;
+      } else {
+        const int h = q - HR * VB * kTile;
+        cc = 0;
+        u = h % VB;
+        rr = h / VB;
+      }
+#else
       const int cc = q % HC, rest = q / HC;
       const int u = rest % VB, rr = rest / VB;  // halo-shifted (row 0 = i0-1, col 0 = j0-1)
+#endif
       const int i = i0 + rr - 1, j = j0 + cc - 1;
       const int vq = chunk * VB + u;
       if (vq >= V || i < 0 || j < 0 || i >= N || j >= N) continue;

@@ -59,12 +59,13 @@ def _worker(conn, d, shape):
             conn.send("bound")
             continue
         out = []
+        t0 = time.perf_counter()
         for i, qv in msg[1]:
             b, Atb, st = nodes[i]
             D, c = ns.assemble(qv, N * N)
             diag = ns.node_update(A, Atb, b, D, c, qv, st, N, prm, dtype=dtype, AT=AT)
             out.append((i, st.x, diag))
-        conn.send(out)
+        conn.send((out, time.perf_counter() - t0))
 
 
 class NodePool:
@@ -119,14 +120,18 @@ class NodePool:
         busy = [w for w, t in enumerate(per) if t]
         for w in busy:
             self._conns[w].send(("update", per[w]))
-        got = {}
+        got, busy_s = {}, []
+        t0 = time.perf_counter()
         for w in busy:
-            for i, x, d in self._conns[w].recv():
+            out, dt = self._conns[w].recv()
+            busy_s.append(dt)
+            for i, x, d in out:
                 got[i] = (x, d)
         self._iters += 1
         if self.verbose:
             print(f"oracle iteration {self._iters}: {len(tasks)} node updates, "
-                  f"{time.perf_counter() - self._t0:.1f} s since bind", flush=True)
+                  f"{time.perf_counter() - self._t0:.1f} s since bind (this one {time.perf_counter() - t0:.1f} s; "
+                  f"worker compute {min(busy_s):.1f}-{max(busy_s):.1f} s)", flush=True)
         return [got[i] for i, _ in tasks]
 
     def close(self):
