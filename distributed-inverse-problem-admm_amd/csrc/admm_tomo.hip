@@ -563,6 +563,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 
   double* redH = (double*)C->redH.p;
   const dim3 tg = tile_grid(C, nch, VB);
   const dim3 cgg((N + kTile - 1) / kTile, (N + kCgRows - 1) / kCgRows, nch);
+  const dim3 tvg((N + kTvTile - 1) / kTvTile, (N + TvMap<VB>::TI - 1) / TvMap<VB>::TI, nch);  // k_tv_update
   const int Pb = C->P_back;
 
   // (D as interleaved samples for the CG operator, dsumS, is packed once at bind time)
@@ -674,7 +675,7 @@ int enqueue_update(admm_ctx* C, hipStream_t s, bool reuse = false, int rounds = 
     double* dout = uout ? ((t % 2) ? ub : ua) : (Tt > 1 ? B.d : dnxt);
     double* eout = uout ? nullptr : (Tt > 1 ? B.e : enxt);
 #define TV_LAUNCH(LASTV, FUSEV, UINV, UOUTV)                                                                     \
-  hipLaunchKernelGGL((k_tv_update<T, VB, LASTV, FUSEV, UINV, UOUTV>), tg, dim3(kBlock), 0, s, xcur, din, ein, dout, \
+  hipLaunchKernelGGL((k_tv_update<T, VB, LASTV, FUSEV, UINV, UOUTV>), tvg, dim3(kTvThreads), 0, s, xcur, din, ein, dout, \
                      eout, r, pout, poutT, tau, B.mu, B.tv_kind, N, V, xnxt, pr, Hp, redH)
     if (!last) {
       if (uin) TV_LAUNCH(false, true, true, true);

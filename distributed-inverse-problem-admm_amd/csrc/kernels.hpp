@@ -2362,8 +2362,39 @@ struct PRing {
 // drops by 4 of its ~34 bytes per node-pixel read+written.  UIN: din holds u (ein unused);
 // UOUT: dout receives u (eout unused).  The x-update's first round reads d, e and its last
 // writes them, so the state between x-updates (and every other kernel) is unchanged.
+// Tile of the TV update: kTvTile columns x kTile / VB rows of VB nodes, kTvThreads threads
+// (ADMM_TV_TW = 64: twice the columns per halo column pair, 512 threads -- fewer partial-line
+// requests per pixel for the same rows; 32: the elementwise kernels' tile, 256 threads)
+#ifndef ADMM_TV_TW
+#define ADMM_TV_TW 64
+#endif
+constexpr int kTvTile = ADMM_TV_TW;
+constexpr int kTvThreads = kTvTile == 64 ? 512 : 256;
+static_assert(kTvTile == 32 || kTvTile == 64, "TV tile width 32 or 64");
+template <int VB>
+struct TvMap {
+  static constexpr int TI = kTile / VB;                       // tile rows
+  static constexpr int RPI = kTvThreads / (kTvTile * VB);     // rows per iteration
+  int u, jj, isub;
+  __device__ TvMap() : u(threadIdx.x % VB), jj((threadIdx.x / VB) % kTvTile), isub(threadIdx.x / (kTvTile * VB)) {}
+};
+template <typename T, int VB>
+struct TvTile {
+  T t[TvMap<VB>::TI][kTvTile + 1][VB];
+};
+// outT[j][i][u] = tile[i - i0][j - j0][u] (as tile_store_T, for the TV tile)
+template <typename T, int VB>
+__device__ __forceinline__ void tv_tile_store_T(TvTile<T, VB>& tl, T* __restrict__ outT, int N, int i0, int j0) {
+  constexpr int TI = TvMap<VB>::TI;
+  __syncthreads();
+  const int u = threadIdx.x % VB, r = (threadIdx.x / VB) % TI, c0 = threadIdx.x / (VB * TI);
+  for (int c = c0; c < kTvTile; c += kTvThreads / (VB * TI)) {
+    const int jj = j0 + c, ii = i0 + r;
+    if (jj < N && ii < N) outT[((size_t)jj * N + ii) * VB + u] = tl.t[r][c][u];
+  }
+}
 template <typename T, int VB, bool LAST, bool FUSE = false, bool UIN = false, bool UOUT = false>
-__global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__ x, const double* __restrict__ din,
+__global__ __launch_bounds__(kTvThreads) void k_tv_update(const double* __restrict__ x, const double* __restrict__ din,
                                                       const double* __restrict__ ein, double* __restrict__ dout,
                                                       double* __restrict__ eout, double* __restrict__ r,
                                                       T* __restrict__ p, T* __restrict__ pT, double tau,
@@ -2371,19 +2402,19 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
                                                       PRing<T> pr, const T* __restrict__ Hp,
                                                       const double* __restrict__ redH) {
   static_assert(!(LAST && UOUT), "the last round writes d and e");
-  __shared__ TileT<T, VB> tl;
-  const EwMap<VB> mp;
+  __shared__ TvTile<T, VB> tl;
+  const TvMap<VB> mp;
   const int chunk = blockIdx.z, v = chunk * VB + mp.u;
   const bool live = v < V;
   const int npix = N * N;
   const size_t sbase = (size_t)chunk * npix * VB;
   const int wg = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
-  const int i0 = (wg / gridDim.x) * EwMap<VB>::TI, j0 = (wg % gridDim.x) * kTile;
+  const int i0 = (wg / gridDim.x) * TvMap<VB>::TI, j0 = (wg % gridDim.x) * kTvTile;
   // FUSE: x after the round's CG steps over the block's stencil region (rows i0-1 .. i0+TI,
-  // columns j0-1 .. j0+kTile), formed once per pixel into LDS from the old x and the p ring
+  // columns j0-1 .. j0+kTvTile), formed once per pixel into LDS from the old x and the p ring
   // (32-B vector loads of each p), x = fma(alpha_k, p_k, x) for k = 0 .. K-1 as the CG
   // updates did it; the stencil then reads LDS only
-  constexpr int PR = EwMap<VB>::TI + 2, PC = kTile + 2;
+  constexpr int PR = TvMap<VB>::TI + 2, PC = kTvTile + 2;
   __shared__ double al_s[FUSE ? kMaxCgRing : 1][VB];
   __shared__ double x_s[FUSE ? VB : 1][FUSE ? PR : 1][FUSE ? PC + 1 : 1];
   if constexpr (FUSE) {
@@ -2397,16 +2428,16 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
       al_s[k][u] = alpha;
     }
     __syncthreads();
-    for (int q = threadIdx.x; q < PR * PC; q += kBlock) {
+    for (int q = threadIdx.x; q < PR * PC; q += kTvThreads) {
 #if ADMM_TV_ALIGN
-      // the tile's kTile columns first (rows of 256-B-aligned float64 runs per node), the two
+      // the tile's kTvTile columns first (rows of 256-B-aligned float64 runs per node), the two
       // halo columns after them: no lane group straddles a cache line
       int rr, cc;
-      if (q < PR * kTile) {
-        rr = q / kTile;
-        cc = 1 + q % kTile;
+      if (q < PR * kTvTile) {
+        rr = q / kTvTile;
+        cc = 1 + q % kTvTile;
       } else {
-        const int h = q - PR * kTile;
+        const int h = q - PR * kTvTile;
         rr = h >> 1;
         cc = (h & 1) ? PC - 1 : 0;
       }
@@ -2455,20 +2486,20 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
     // keeping q = (d' - e') - (d - e) per component in LDS; tile points also store d', e'.
     // Phase 2: K^T q at each tile pixel from LDS (the same four terms, in the same order,
     // that the neighbour re-evaluation used), then r += mu K^T q, p = r.
-    constexpr int TI = EwMap<VB>::TI, HC = kTile + 1, HR = TI + 1;
+    constexpr int TI = TvMap<VB>::TI, HC = kTvTile + 1, HR = TI + 1;
     // column-fastest: a wave reads runs of 33 consecutive pixels of one node
     __shared__ double qx_s[HR][VB][HC], qy_s[HR][VB][HC];
-    for (int q = threadIdx.x; q < HR * HC * VB; q += kBlock) {
+    for (int q = threadIdx.x; q < HR * HC * VB; q += kTvThreads) {
 #if ADMM_TV_ALIGN
-      // (as above: the kTile tile columns of every (row, node) first, the halo column after)
+      // (as above: the kTvTile tile columns of every (row, node) first, the halo column after)
       int cc, u, rr;
-      if (q < HR * VB * kTile) {
-        cc = 1 + q % kTile;
-        const int rest = q / kTile;
+      if (q < HR * VB * kTvTile) {
+        cc = 1 + q % kTvTile;
+        const int rest = q / kTvTile;
         u = rest % VB;
         rr = rest / VB;
       } else {
-        const int h = q - HR * VB * kTile;
+        const int h = q - HR * VB * kTvTile;
         cc = 0;
         u = h % VB;
         rr = h / VB;
@@ -2515,7 +2546,7 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
       }
     }
     __syncthreads();
-    for (int rw = mp.isub; rw < TI; rw += EwMap<VB>::RPI) {
+    for (int rw = mp.isub; rw < TI; rw += TvMap<VB>::RPI) {
       const int i = i0 + rw, j = j0 + mp.jj;
       if (i >= N || j >= N) continue;
       const int o = i * N + j;
@@ -2538,10 +2569,10 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
       p[sbase + (size_t)o * VB + mp.u] = sv;
       tl.t[rw][mp.jj][mp.u] = sv;
     }
-    tile_store_T<T, VB>(tl, pT + sbase, N, i0, j0);
+    tv_tile_store_T<T, VB>(tl, pT + sbase, N, i0, j0);
     return;
   }
-  for (int rw = mp.isub; rw < EwMap<VB>::TI; rw += EwMap<VB>::RPI) {
+  for (int rw = mp.isub; rw < TvMap<VB>::TI; rw += TvMap<VB>::RPI) {
     const int i = i0 + rw, j = j0 + mp.jj;
     if (i >= N || j >= N) continue;
     const int o = i * N + j;
@@ -2575,7 +2606,7 @@ __global__ __launch_bounds__(kBlock) void k_tv_update(const double* __restrict__
     p[sbase + (size_t)o * VB + mp.u] = sv;
     tl.t[rw][mp.jj][mp.u] = sv;
   }
-  tile_store_T<T, VB>(tl, pT + sbase, N, i0, j0);
+  tv_tile_store_T<T, VB>(tl, pT + sbase, N, i0, j0);
 }
 
 // node-major float64 [V][L] -> interleaved samples [C][L][VB] of type T  (grid.y = chunk)

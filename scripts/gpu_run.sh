@@ -63,7 +63,7 @@ for step in "$@"; do
     profvar=*)  # profvar=NAME: rocprofv3 kernel stats of the headline with variants/lib_NAME.so ("base": in-tree)
       v=${step#profvar=}; lib=variants/lib_$v.so; [ $v = base ] && lib=
       ADMM_TOMO_LIB=$lib run $step 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profvar_${v}_${TAG} -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --headline-only > gpurun_out/profvar_${v}_${TAG}.log 2>&1 || exit 1
-      python scripts/top_kernels.py gpurun_out/profvar_${v}_${TAG} | head -8 ;;
+      python scripts/top_kernels.py gpurun_out/profvar_${v}_${TAG} > gpurun_out/profvar_${v}_${TAG}.txt; head -8 gpurun_out/profvar_${v}_${TAG}.txt ;;
     bench)
       run bench 600 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || { tail -5 gpurun_out/bench_${TAG}.err; exit 1; }
       python scripts/summarize_bench.py gpurun_out/bench_${TAG}.json ;;
