@@ -958,7 +958,7 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
   }
   // the float taps' kf_split needs k_f + kbias in (0, 2^20) for every pixel and angle (the sum
   // with 2^20 must stay in [2^20, 2^21)); a detector far off the image could break that
-  for (int t = 0; t < g.n_angles; ++t) {
+  for (int t = 0; t < g.n_angles && dtype == ADMM_DTYPE_F32; ++t) {
     const double kmx = C->Kb + C->kbias + c0 * (std::fabs(ba[t].Bi) + std::fabs(ba[t].Bj)) + 2.0;
     if (kmx >= 1048576.0) {
       delete C;  // (nothing allocated on the device yet)

@@ -96,6 +96,20 @@ def test_finer_detector_rejected(cuda):
         RayTransform(ParallelBeamGeometry(32, 10, det_width_factor=0.5)) @ np.zeros(1024)
 
 
+def test_far_off_detector_rejected_by_the_float_taps_range(cuda):
+    """admm_ctx_create refuses a geometry whose bin positions reach 2^20 (the float back
+    projector's biased k_f, kernels.hpp kf_split) instead of addressing garbage."""
+    import ctypes as C
+    lib = _lib.load()
+    h = C.c_void_p()
+    far = _lib.Geom(32, 10, 32, 0, 0.0, float(np.pi), -2.0e6 - 2.0, -2.0e6)  # k_f ~ 3.2e7
+    with pytest.raises(_lib.AdmmError, match="2\\^20"):
+        _lib.check(lib.admm_ctx_create(C.byref(h), C.byref(far), _lib.ADMM_DTYPE_F32, 1, 0), "admm_ctx_create")
+    ok = _lib.Geom(32, 10, 32, 0, 0.0, float(np.pi), -1.0, 1.0)
+    _lib.check(lib.admm_ctx_create(C.byref(h), C.byref(ok), _lib.ADMM_DTYPE_F32, 1, 0), "admm_ctx_create")
+    _lib.check(lib.admm_ctx_destroy(h), "admm_ctx_destroy")
+
+
 @pytest.mark.parametrize("N", [2, 33, 64])
 def test_tv_stencils_match_oracle(cuda, N):
     import ctypes as C
