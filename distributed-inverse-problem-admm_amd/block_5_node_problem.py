@@ -16,15 +16,15 @@ use (block_6_admm_loop_ver2.py:97-135, test_block5_with_aggregate.py:59-73):
 Repeated calls are cheap: the reference builds a new problem for every node
 in every outer iteration (block_6_admm_loop_ver2.py:97) and only the targets v_ij change
 between them.  The device batch of a node is therefore cached across calls, keyed on the
-operator and sinogram objects (``Ai``, ``bi`` -- the reference passes ``A_dense_list[i]``,
-``b[i]``), the neighbour count and the solve configuration; a later call copies its v_ij into
+operator object ``Ai`` (the reference passes ``A_dense_list[i]``), a digest of the sinogram
+``bi``'s bytes, the neighbour count and the solve configuration; a later call copies its v_ij into
 the batch's z rows, re-binds only when the precisions q_ij changed in value (D = sum q is
 setup data of the bound batch), and replays the recorded x-update.  ``solve(warm_start=True)``
 (the reference's own keyword, :123) starts from that node's previous x and split-Bregman state
 -- a documented deviation: CVXPY's warm start of a freshly built problem starts from nothing;
 ``warm_start=False`` starts from x = 0, d = e = 0 and gives bitwise the uncached result.
-``CACHE_ENTRIES`` bounds the cache (least recently used batch dropped); ``clear_cache()``
-frees it.
+``CACHE_ENTRIES`` and ``CACHE_BYTES`` (an estimate of the batches' device memory) bound the cache
+(least recently used batch dropped first); ``clear_cache()`` frees it.
 
 The objective is 0.5||Ai x - bi||^2 + lam_tv TV(x) + sum_j rho/2 ||x - v_ij||^2_Qij
 (:21-29), with textbook isotropic TV (the reference's
@@ -32,6 +32,7 @@ CVXPY atom mis-pairs its differences; documented deviation).
 """
 from __future__ import annotations
 
+import hashlib
 import math
 from collections import OrderedDict
 from types import SimpleNamespace
@@ -72,6 +73,7 @@ def _star_plan(deg: int) -> ShardPlan:
 
 
 CACHE_ENTRIES = 256  # bound node batches kept across build_node_problem calls (0: no cache)
+CACHE_BYTES = 16 << 30  # ... and their estimated device memory
 _CACHE: "OrderedDict[tuple, _Entry]" = OrderedDict()
 
 
@@ -83,10 +85,11 @@ def clear_cache() -> None:
 class _Entry:
     """A bound one-node batch, the objects its key names and the q_ij it was bound with."""
 
-    def __init__(self, nb, refs, qhost):
+    def __init__(self, nb, refs, qhost, nbytes):
         self.nb = nb
-        self.refs = refs    # (Ai, bi) as passed: keeps the key's object ids valid while cached
+        self.refs = refs    # (Ai,): keeps the key's object id valid while cached
         self.qhost = qhost  # float64 host copies of the q_ij in the batch
+        self.nbytes = nbytes
 
 
 def _host64(v, n, what):
@@ -124,7 +127,9 @@ class _Problem:
         self.solver_stats = SimpleNamespace(num_iters=None, solver_name="admm_hip")
 
     def _key(self, cfg):
-        return (id(self.A0), id(self.b), len(self.v), cfg, self.rho, self.lam, self.N)
+        b = self.b.detach().to("cpu").numpy() if isinstance(self.b, torch.Tensor) else np.asarray(self.b)
+        bd = hashlib.blake2b(np.ascontiguousarray(b).tobytes(), digest_size=16).hexdigest()
+        return (id(self.A0), bd, str(b.dtype), len(self.v), cfg, self.rho, self.lam, self.N)
 
     def _build(self, cfg, qhost):
         tv_iters, cg_iters, mu, tv_kind = cfg
@@ -140,7 +145,7 @@ class _Problem:
         qhost = [_host64(q, n, "q vector") for q in self.q]
         key = self._key(cfg)
         ent = _CACHE.get(key) if CACHE_ENTRIES > 0 else None
-        if ent is not None and ent.refs[0] is self.A0 and ent.refs[1] is self.b:
+        if ent is not None and ent.refs[0] is self.A0:
             _CACHE.move_to_end(key)
             nb = ent.nb
             if any(not np.array_equal(a, b) for a, b in zip(qhost, ent.qhost)):
@@ -153,8 +158,11 @@ class _Problem:
         else:
             nb = self._build(cfg, qhost)
             if CACHE_ENTRIES > 0:
-                _CACHE[key] = _Entry(nb, (self.A0, self.b), qhost)
-                while len(_CACHE) > CACHE_ENTRIES:
+                # (estimate: float64 x_ext, d, e, r, c, A^T b, D, z, y, q rows and ~16 sample vectors)
+                nbytes = 8 * n * (3 * len(self.v) + 12) + 4 * n * 16
+                _CACHE[key] = _Entry(nb, (self.A0,), qhost, nbytes)
+                while len(_CACHE) > CACHE_ENTRIES or (
+                        len(_CACHE) > 1 and sum(e.nbytes for e in _CACHE.values()) > CACHE_BYTES):
                     _CACHE.popitem(last=False)
         for e, v in enumerate(self.v):
             nb.z[e].copy_(torch.as_tensor(np.asarray(v) if not isinstance(v, torch.Tensor) else v)

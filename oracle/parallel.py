@@ -8,8 +8,8 @@ processes gives exactly the sequential loop's results.
 Layout (cheap enough that whole C2/C3 trajectories fit the GPU suite's budget):
 
 * the Joseph CSR matrix and its transpose are built ONCE, in this process, and written as
-  ``.npy`` arrays to a scratch directory; every worker memory-maps them (one copy in the
-  page cache, no per-worker rebuild);
+  ``.npy`` arrays to a scratch directory; every worker reads them into its own memory (no
+  per-worker rebuild; private pages keep the SpMVs on the worker's NUMA node);
 * node i lives in worker ``i % procs`` for the whole trajectory: its b_i, A^T b_i and
   split-Bregman ``NodeState`` never cross a pipe after ``bind``;
 * per iteration a worker receives only its nodes' (q_ij, v_ij) lists and returns only x_i
@@ -36,16 +36,21 @@ def _save_csr(M, d, name):
         np.save(os.path.join(d, f"{name}_{p}.npy"), getattr(M, p))
 
 
-def _load_csr(d, name, shape):
+def _load_csr(d, name, shape, private=False):
+    """The saved CSR matrix, memory-mapped -- or (``private``) read into this process's own
+    memory: first-touched by the worker, so on a multi-socket host its pages sit on the worker's
+    NUMA node instead of wherever the shared page cache put them (the C3 pool's x-updates ran at
+    5.7-7.8 s per node from the shared mapping on the GPU box, against 2.6 s in bench.py's
+    private-matrix workers)."""
     import scipy.sparse as sp
-    arr = [np.load(os.path.join(d, f"{name}_{p}.npy"), mmap_mode="r") for p in _PARTS]
+    arr = [np.load(os.path.join(d, f"{name}_{p}.npy"), mmap_mode=None if private else "r") for p in _PARTS]
     return sp.csr_matrix(tuple(arr), shape=shape)
 
 
 def _worker(conn, d, shape):
     from . import node_solver as ns
-    A = _load_csr(d, "A", shape)
-    AT = _load_csr(d, "AT", shape[::-1])
+    A = _load_csr(d, "A", shape, private=True)
+    AT = _load_csr(d, "AT", shape[::-1], private=True)
     nodes = {}  # i -> (b_i, A^T b_i, NodeState)
     prm = N = dtype = None
     conn.send("ready")
