@@ -1445,36 +1445,45 @@ constexpr int kBAngC = ADMM_BK_ANGC;  // angles per staged sinogram-window chunk
 // per node, x over the tile plus one halo row/column on each side is staged in LDS and
 // the TV subgradient of every point (tile + the halo row/column above/left) is computed
 // ONCE into LDS -- the per-pixel form evaluated it at three points and re-read x nine
-// times.  `scratch`: (kBTI+2)(kBTJ+2) + 2 (kBTI+1)(kBTJ+1) doubles of LDS.
+// times.  kDiagG nodes per pass (round 6: their x tiles load in one loop, one third of the
+// barriers); `scratch`: kDiagScratch doubles of LDS.
+#ifndef ADMM_DIAG_G
+#define ADMM_DIAG_G 2
+#endif
+constexpr int kDiagG = ADMM_DIAG_G;  // nodes per staging pass of the DIAG epilogue
+constexpr int kDiagScratch = kDiagG * ((kBTI + 2) * (kBTJ + 2) + 2 * (kBTI + 1) * (kBTJ + 1));
 template <typename T, int VB, int VS = VB>
 __device__ __forceinline__ void diag_epilogue_tile(const BackArgs<T>& A, double* scratch, int ib, int jb, int i,
                                                    int j, bool inb, int chunk, int v0, int nv, const T (&acc)[VB],
                                                    double (&pq)[VB][5], int lo = 0) {
   constexpr int XC = kBTJ + 2, XR = kBTI + 2, SC = kBTJ + 1, SR = kBTI + 1;
-  double* xt = scratch;            // [XR][XC]: rows ib-1 .. ib+kBTI, cols jb-1 .. jb+kBTJ
-  double* sx = xt + XR * XC;       // [SR][SC]: subgradient at rows ib-1 .. ib+kBTI-1, cols jb-1 ..
-  double* sy = sx + SR * SC;
+  constexpr int G = kDiagG, XS = XR * XC, SS = SR * SC;
+  // per node g of a pass: xt = scratch + g XS  [XR][XC]: rows ib-1 .. ib+kBTI, cols jb-1 .. jb+kBTJ;
+  // sx, sy = scratch + G XS + 2 g SS (+ SS)  [SR][SC]: subgradient at rows ib-1 .., cols jb-1 ..
   const int N = A.N, npix = N * N;
   const int pix = i * N + j;
   const size_t sbase = (size_t)chunk * npix * VS + lo;
   if (inb && A.out_t) gstore<T, VB>(A.out_t + sbase + (size_t)pix * VS, acc);
   const int ti = i - ib + 1, tj = j - jb + 1;  // this pixel in the staged x tile
 #pragma unroll
-  for (int u = 0; u < VB; ++u) {  // constant bounds keep acc / pq in registers
-    if (u >= nv) break;           // block-uniform: the barriers below stay uniform
-    const int v = v0 + u;
-    const size_t vo = (size_t)v * npix;
-    const double* xv = A.x + vo;
-    __syncthreads();  // previous node's (or the tap loop's) LDS readers are done
-    for (int q = threadIdx.x; q < XR * XC; q += kBkThreads) {
-      const int rr = q / XC, cc = q % XC;
+  for (int u0 = 0; u0 < VB; u0 += G) {  // constant bounds keep acc / pq in registers
+    if (u0 >= nv) break;                // block-uniform: the barriers below stay uniform
+    const int ng = min(G, nv - u0);
+    __syncthreads();  // previous pass's (or the tap loop's) LDS readers are done
+    // the pass's G x tiles in one loop: their global loads are in flight together
+    for (int q = threadIdx.x; q < ng * XS; q += kBkThreads) {
+      const int g = q / XS, e = q % XS;
+      const int rr = e / XC, cc = e % XC;
       const int ii = ib - 1 + rr, jj = jb - 1 + cc;
-      xt[q] = (ii >= 0 && jj >= 0 && ii < N && jj < N) ? xv[ii * N + jj] : 0.0;
+      const double* xv = A.x + (size_t)(v0 + u0 + g) * npix;
+      scratch[q] = (ii >= 0 && jj >= 0 && ii < N && jj < N) ? xv[ii * N + jj] : 0.0;
     }
     __syncthreads();
-    for (int q = threadIdx.x; q < SR * SC; q += kBkThreads) {
-      const int rr = q / SC, cc = q % SC;
+    for (int q = threadIdx.x; q < ng * SS; q += kBkThreads) {
+      const int g = q / SS, e = q % SS;
+      const int rr = e / SC, cc = e % SC;
       const int ii = ib - 1 + rr, jj = jb - 1 + cc;
+      const double* xt = scratch + g * XS;
       double px = 0.0, py = 0.0;
       if (ii >= 0 && jj >= 0 && ii < N && jj < N) {
         const double c = xt[rr * XC + cc];
@@ -1482,46 +1491,56 @@ __device__ __forceinline__ void diag_epilogue_tile(const BackArgs<T>& A, double*
         const double gy = (jj < N - 1) ? xt[rr * XC + cc + 1] - c : 0.0;
         tv_sub(gx, gy, A.tv_kind, px, py);
       }
-      sx[q] = px;
-      sy[q] = py;
+      scratch[G * XS + 2 * g * SS + e] = px;
+      scratch[G * XS + (2 * g + 1) * SS + e] = py;
     }
     __syncthreads();
     if (!inb) continue;
-    const double xc = xt[ti * XC + tj];
-    const double gx = (i < N - 1) ? xt[(ti + 1) * XC + tj] - xc : 0.0;
-    const double gy = (j < N - 1) ? xt[ti * XC + tj + 1] - xc : 0.0;
-    const double tvv = (A.tv_kind == 0) ? sqrt(gx * gx + gy * gy) : fabs(gx) + fabs(gy);
-    // lam * K^T sub(Kx) at (i,j): subgradients at (i,j), (i-1,j), (i,j-1)
-    double kts = 0.0;
-    if (i <= N - 2) kts -= sx[ti * SC + tj];
-    if (j <= N - 2) kts -= sy[ti * SC + tj];
-    if (i >= 1) kts += sx[(ti - 1) * SC + tj];
-    if (j >= 1) kts += sy[ti * SC + tj - 1];
-    const double cc = A.cvec[vo + pix];
-    const double sm = (double)acc[u] + A.rho * (A.dsum[vo + pix] * xc - cc);  // gradient of the quadratic
-    const double g = sm + A.lam * kts;
-    // K^T e at (i, j) (e = final Bregman variable [2][n] of node v)
-    const double* ev = A.evar + 2 * vo;
-    double kte = 0.0;
-    if (i >= 1) kte += ev[pix - N];
-    if (i <= N - 2) kte -= ev[pix];
-    if (j >= 1) kte += ev[npix + pix - 1];
-    if (j <= N - 2) kte -= ev[npix + pix];
-    const double rsb = sm + A.mu * kte;
-    double quad = 0.0;
-    for (int q = A.inc_off[v]; q < A.inc_off[v + 1]; ++q) {
-      const double vij = edge_v(A.edges, A.inc_edge[q], A.inc_sign[q], npix, pix);
-      const double dd = xc - vij;
-      quad += A.qv[(size_t)A.inc_qslot[q] * npix + pix] * dd * dd;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int u = u0 + g;
+      if (u >= VB || g >= ng) break;
+      const int v = v0 + u;
+      const size_t vo = (size_t)v * npix;
+      const double* xt = scratch + g * XS;
+      const double* sx = scratch + G * XS + 2 * g * SS;
+      const double* sy = sx + SS;
+      const double xc = xt[ti * XC + tj];
+      const double gx = (i < N - 1) ? xt[(ti + 1) * XC + tj] - xc : 0.0;
+      const double gy = (j < N - 1) ? xt[ti * XC + tj + 1] - xc : 0.0;
+      const double tvv = (A.tv_kind == 0) ? sqrt(gx * gx + gy * gy) : fabs(gx) + fabs(gy);
+      // lam * K^T sub(Kx) at (i,j): subgradients at (i,j), (i-1,j), (i,j-1)
+      double kts = 0.0;
+      if (i <= N - 2) kts -= sx[ti * SC + tj];
+      if (j <= N - 2) kts -= sy[ti * SC + tj];
+      if (i >= 1) kts += sx[(ti - 1) * SC + tj];
+      if (j >= 1) kts += sy[ti * SC + tj - 1];
+      const double cc = A.cvec[vo + pix];
+      const double sm = (double)acc[u] + A.rho * (A.dsum[vo + pix] * xc - cc);  // gradient of the quadratic
+      const double gg = sm + A.lam * kts;
+      // K^T e at (i, j) (e = final Bregman variable [2][n] of node v)
+      const double* ev = A.evar + 2 * vo;
+      double kte = 0.0;
+      if (i >= 1) kte += ev[pix - N];
+      if (i <= N - 2) kte -= ev[pix];
+      if (j >= 1) kte += ev[npix + pix - 1];
+      if (j <= N - 2) kte -= ev[npix + pix];
+      const double rsb = sm + A.mu * kte;
+      double quad = 0.0;
+      for (int q = A.inc_off[v]; q < A.inc_off[v + 1]; ++q) {
+        const double vij = edge_v(A.edges, A.inc_edge[q], A.inc_sign[q], npix, pix);
+        const double dd = xc - vij;
+        quad += A.qv[(size_t)A.inc_qslot[q] * npix + pix] * dd * dd;
+      }
+      pq[u][0] += gg * gg;
+      pq[u][1] += tvv;
+      pq[u][2] += 0.5 * A.rho * quad;
+      if (A.phantom) {
+        const double dp = xc - A.phantom[pix];
+        pq[u][3] += dp * dp;
+      }
+      pq[u][4] += rsb * rsb;
     }
-    pq[u][0] += g * g;
-    pq[u][1] += tvv;
-    pq[u][2] += 0.5 * A.rho * quad;
-    if (A.phantom) {
-      const double dp = xc - A.phantom[pix];
-      pq[u][3] += dp * dp;
-    }
-    pq[u][4] += rsb * rsb;
   }
 }
 
@@ -1796,7 +1815,7 @@ void k_back(BackArgs<T> A) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) pq[u][q] = 0.0;
   if constexpr (MODE == BACK_DIAG) {
-    __shared__ double diag_s[(kBTI + 2) * (kBTJ + 2) + 2 * (kBTI + 1) * (kBTJ + 1)];
+    __shared__ double diag_s[kDiagScratch];
     diag_epilogue_tile<T, VB>(A, diag_s, ib, jb, i, j, inb, chunk, v0, nv, acc, pq);
   } else if (inb) {
     back_epilogue<T, VB, MODE, NQ>(A, i, j, chunk, v0, nv, acc, pq);
@@ -2054,7 +2073,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) pq[u][q] = 0.0;
   if constexpr (MODE == BACK_DIAG) {
-    __shared__ double diag_s[(kBTI + 2) * (kBTJ + 2) + 2 * (kBTI + 1) * (kBTJ + 1)];
+    __shared__ double diag_s[kDiagScratch];
     diag_epilogue_tile<T, MH, VBR>(A, diag_s, ib, jb, i, j, inb, rc, v0, nv, r1, pq, mq * MH);
     diag_epilogue_tile<T, MH, VBR>(A, diag_s, N - ib - kBTI, jb, i2, j, inb2, rc, v0, nv, r2, pq, mq * MH);
   } else {
