@@ -199,10 +199,13 @@ def decentralized_admm(ops, sinograms, G, Qij_diag_fn, N, lam_tv=0.01, rho=1.0,
             g_i[i] = d.g_norm
             mse_i[i] = d.mse_sino
         if threads is not None and threads > 1 and tasks:
+            def update(task):  # one node's x-update (its own state; products serialized)
+                i, qv = task
+                D, c = ns.assemble(qv, n)
+                return ns.node_update(ops[i], Atb[i], b[i], D, c, qv, states[i], N, prm, dtype=dtype, AT=ATs[i])
+
             with ThreadPoolExecutor(threads) as ex:
-                done = list(ex.map(lambda t: ns.node_update(ops[t[0]], Atb[t[0]], b[t[0]], *ns.assemble(t[1], n),
-                                                            t[1], states[t[0]], N, prm, dtype=dtype,
-                                                            AT=ATs[t[0]]), tasks))
+                done = list(ex.map(update, tasks))
             for (i, _), d in zip(tasks, done):
                 nu_i[i] = 1
                 obj_i[i], sb_i[i], g_i[i], mse_i[i] = d.obj, d.sb_res, d.g_norm, d.mse_sino

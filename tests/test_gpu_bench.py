@@ -104,12 +104,16 @@ def test_bench_as_rank_share(cuda):
 @pytest.mark.long
 @pytest.mark.timeout(600)
 def test_bench_default_proxies(cuda):
-    """The default one-GPU line's per-rank proxies: C3 on 2 ranks, C4 on 2 / 4 / 8 ranks, each
-    with its measured one-GPU time, the share's time and the predicted speedup.  (ADMM_TEST_LONG:
+    """The default one-GPU line's per-rank proxies: C3 on 2 ranks, C4 on 2 / 4 / 8 ranks, C5 on 8
+    and the weak headline on 8, each with its measured one-GPU time, the share's time and the
+    predicted speedup.  (ADMM_TEST_LONG:
     the driver's own default bench run produces this line every round.)"""
     b = _run("--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--strong-steps", "1", "--proxy-steps", "1")
     px = b["proxy_8gpu"]
-    assert set(k for k in px if "@" in k) == {"C3@2", "C4@2", "C4@4", "C4@8"}
+    assert set(k for k in px if "@" in k) == {"C3@2", "C4@2", "C4@4", "C4@8", "C5@8", "weak8@8"}
+    w = px["weak8@8"]  # the N = 8 weak headline: 64 nodes, 8 per rank
+    assert w["nodes"] == 64 and w["shares"][0]["local_nodes"] == 8 and w["predicted_speedup"] > 0
+    assert abs(w["predicted_value"] - 64e3 / w["predicted_ms_per_step"]) < 1e-6 * w["predicted_value"]
     assert [s["config"] for s in b["strong"]] == ["C4"]
     for k in ("C3@2", "C4@2", "C4@4", "C4@8"):
         p = px[k]
