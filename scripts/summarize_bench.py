@@ -19,6 +19,11 @@ for s in b.get("strong", []):
 for k, p in sorted(b.get("proxy_8gpu", {}).items()):
     if not isinstance(p, dict):
         continue
+    if "T1_ms_per_step" not in p:  # weak8@8: the N = 8 weak headline itself
+        print(f"proxy {k}: {p['nodes']} nodes on {p['ranks']} ranks, predicted {p['predicted_value']:.0f} "
+              f"node-updates/s ({p['predicted_ms_per_step']:.2f} ms/step), {p['predicted_speedup']:.2f}x the "
+              f"one-GPU headline (one link {p['predicted_speedup_one_link']:.2f}x)")
+        continue
     sh = " | ".join(f"r{s['rank']}: V={s['local_nodes']} vb={s['vb']} H={s['halo_rows']} E={s['stored_edges']} "
                     f"{s['ms_per_step']:.2f} ms (cons {s.get('consensus_ms', float('nan')):.2f}) + ex "
                     f"{s['exchange'].get('ms_conservative', s['exchange']['ms_direct']):.2f} ({s['exchange']['mode']}) "
