@@ -220,13 +220,12 @@ __device__ __forceinline__ void block_reduce(double (&v)[NQ], double* lds /* >= 
 // the NW waves are combined in LDS in a fixed pairwise tree.  On return thread t < NV of the
 // block can read total t from out_lds[t].  Fixed order -> bitwise reproducible.
 // ---------------------------------------------------------------------------
-template <int NV, int NW = 4>
-__device__ __forceinline__ void block_reduce_rs(double (&v)[NV], double* lds /* >= NW*NV */,
-                                                double* out_lds /* >= NV */) {
-  static_assert(NW == 4 || NW == 8 || NW == 16, "NW = 4, 8 or 16 waves");
+// the wave part: on return the lanes with (lane & 3) == 0 hold NV / 16 wave totals each, of
+// the values base .. base + NV/16 - 1 (base returned)
+template <int NV>
+__device__ __forceinline__ int wave_rs(double (&v)[NV]) {
   static_assert(NV % 16 == 0, "NV must be a multiple of 16");
   const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
   // at offsets 32 and 16: after the swap, lane i of x + y is (keep + partner's send), with no
   // LDS traffic and no selects
 #pragma unroll
@@ -262,26 +261,157 @@ __device__ __forceinline__ void block_reduce_rs(double (&v)[NV], double* lds /* 
     s += dpp_d<0xB1>(s);
     v[k] = s;
   }
-  if ((lane & 3) == 0) {
-    const int base = ((lane >> 5) & 1) * (NV / 2) + ((lane >> 4) & 1) * (NV / 4) + ((lane >> 3) & 1) * (NV / 8) +
-                     ((lane >> 2) & 1) * (NV / 16);
+  return ((lane >> 5) & 1) * (NV / 2) + ((lane >> 4) & 1) * (NV / 4) + ((lane >> 3) & 1) * (NV / 8) +
+         ((lane >> 2) & 1) * (NV / 16);
+}
+
+// NB (1, 2, 4 or 8) values: halving exchanges while more than one value remains, then the plain
+// butterfly over the remaining offsets (the same exact-xor pairing at every level, so each total
+// is the full butterfly's bit for bit).  Every lane returns the total of value *idx; the lanes
+// with (lane & (64 / NB - 1)) == 0 are one writer per value.
+template <int NB>
+__device__ __forceinline__ double wave_rs_tail(double (&t)[NB], int& idx) {
+  static_assert(NB == 1 || NB == 2 || NB == 4 || NB == 8, "tail of 1, 2, 4 or 8 values");
+  const int lane = threadIdx.x & 63;
+  if constexpr (NB >= 2) {
 #pragma unroll
-    for (int k = 0; k < NV / 16; ++k) lds[wid * NV + base + k] = v[k];
+    for (int k = 0; k < NB / 2; ++k) {
+      double x = t[k], y = t[NB / 2 + k];
+      permswap_d<true>(x, y);
+      t[k] = x + y;
+    }
   }
-  __syncthreads();
-  if ((int)threadIdx.x < NV) {
+  if constexpr (NB >= 4) {
+#pragma unroll
+    for (int k = 0; k < NB / 4; ++k) {
+      double x = t[k], y = t[NB / 4 + k];
+      permswap_d<false>(x, y);
+      t[k] = x + y;
+    }
+  }
+  double s = t[0];
+  if constexpr (NB >= 8) {
+    const bool h8 = lane & 8;
+    const double send = h8 ? t[0] : t[1], keep = h8 ? t[1] : t[0];
+    s = keep + dpp_d<0x128>(send);
+  }
+  if constexpr (NB < 2) {
+    double x = s, y = s;
+    permswap_d<true>(x, y);
+    s = x + y;
+  }
+  if constexpr (NB < 4) {
+    double x = s, y = s;
+    permswap_d<false>(x, y);
+    s = x + y;
+  }
+  if constexpr (NB < 8) s += dpp_d<0x128>(s);
+  const double up = dpp_d<0x104>(s), dn = dpp_d<0x114>(s);  // xor 4
+  s += (lane & 4) ? dn : up;
+  s += dpp_d<0x4E>(s);
+  s += dpp_d<0xB1>(s);
+  idx = (NB >= 2 ? ((lane >> 5) & 1) * (NB / 2) : 0) + (NB >= 4 ? ((lane >> 4) & 1) * (NB / 4) : 0) +
+        (NB >= 8 ? ((lane >> 3) & 1) * (NB / 8) : 0);
+  return s;
+}
+
+// the NW wave totals of value t (stride NS in lds) combined in a fixed pairwise tree
+template <int NS, int NW>
+__device__ __forceinline__ void block_combine(const double* lds, double* out_lds) {
+  if ((int)threadIdx.x < NS) {
     const int t = threadIdx.x;
-    // fixed pairwise tree over the NW wave totals
     double w[NW];
 #pragma unroll
-    for (int q = 0; q < NW; ++q) w[q] = lds[q * NV + t];
+    for (int q = 0; q < NW; ++q) w[q] = lds[q * NS + t];
 #pragma unroll
     for (int h = NW / 2; h >= 1; h >>= 1)
 #pragma unroll
       for (int q = 0; q < h; ++q) w[q] = w[2 * q] + w[2 * q + 1];
     out_lds[t] = w[0];
   }
+}
+
+// ---------------------------------------------------------------------------
+// deterministic block reduction of NV (multiple of 16) float64 values per thread
+// by a wave-level reduce-scatter butterfly: at offsets 32, 16, 8, 4 every lane
+// keeps half of its values and adds its partner's copy of that half (NV/2 + NV/4
+// + NV/8 + NV/16 exchanges instead of 6*NV), then a plain butterfly over offsets
+// 2, 1 on the last NV/16.  Exchanges are gfx950 permlane32/16 swaps (offsets 32, 16)
+// and DPP row moves (8, 4, 2, 1): every level an exact xor pairing, so the totals are
+// the __shfl_xor butterfly's bit for bit (profiles/r2_reduce_dpp_bitwise.txt).  Lanes with (lane & 3) == 0 then hold the wave totals;
+// the NW waves are combined in LDS in a fixed pairwise tree.  On return thread t < NV of the
+// block can read total t from out_lds[t].  Fixed order -> bitwise reproducible.
+// ---------------------------------------------------------------------------
+template <int NV, int NW = 4>
+__device__ __forceinline__ void block_reduce_rs(double (&v)[NV], double* lds /* >= NW*NV */,
+                                                double* out_lds /* >= NV */) {
+  static_assert(NW == 4 || NW == 8 || NW == 16, "NW = 4, 8 or 16 waves");
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int base = wave_rs<NV>(v);
+  if ((lane & 3) == 0) {
+#pragma unroll
+    for (int k = 0; k < NV / 16; ++k) lds[wid * NV + base + k] = v[k];
+  }
   __syncthreads();
+  block_combine<NV, NW>(lds, out_lds);
+  __syncthreads();
+}
+
+// NA (multiple of 16) + NB (1, 2, 4 or 8) values without padding NA + NB up to a multiple of
+// 16 (round 6: 20 = 16 + 4 CG dot partials of a 4-node back-projector lane block, 42 fewer
+// VALU per thread than the padded 32): each value's total is the same butterfly, bit for bit,
+// and the waves are combined in the same tree, so out_lds[t], t < NA + NB, is block_reduce_rs'
+// result for the padded vector.
+template <int NA, int NB, int NW>
+__device__ __forceinline__ void block_reduce_rs_tail(double (&v)[NA], double (&tb)[NB], double* lds /* >= NW*(NA+NB) */,
+                                                     double* out_lds /* >= NA+NB */) {
+  static_assert(NW == 4 || NW == 8 || NW == 16, "NW = 4, 8 or 16 waves");
+  constexpr int NS = NA + NB;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int base = wave_rs<NA>(v);
+  int ti;
+  const double ts = wave_rs_tail<NB>(tb, ti);
+  if ((lane & 3) == 0) {
+#pragma unroll
+    for (int k = 0; k < NA / 16; ++k) lds[wid * NS + base + k] = v[k];
+  }
+  if ((lane & (64 / NB - 1)) == 0) lds[wid * NS + NA + ti] = ts;
+  __syncthreads();
+  block_combine<NS, NW>(lds, out_lds);
+  __syncthreads();
+}
+
+// The block's NT = NQ x (lane-block nodes) dot partials per thread (pq flattened node-major)
+// reduced to out_lds[0 .. NT): unpadded NA + NB when NT is 16k + 1, 2, 4 or 8 (k >= 1),
+// otherwise padded to a multiple of 16 -- the same totals either way
+#ifndef ADMM_RS_TAIL
+#define ADMM_RS_TAIL 1  // 0: always the padded form (A/B builds)
+#endif
+template <int NT>
+struct RsShape {
+  static constexpr int NA = (NT / 16) * 16, NB = NT - NA;
+  static constexpr bool SPLIT = ADMM_RS_TAIL && NA >= 16 && (NB == 1 || NB == 2 || NB == 4 || NB == 8);
+  static constexpr int NS = SPLIT ? NT : ((NT + 15) / 16) * 16;  // LDS stride / out_lds size
+};
+template <int NT, int NW>
+__device__ __forceinline__ void block_reduce_flat(const double (&vals)[NT], double* lds, double* out_lds) {
+  using S = RsShape<NT>;
+  if constexpr (S::SPLIT) {
+    double fa[S::NA], fb[S::NB];
+#pragma unroll
+    for (int k = 0; k < S::NA; ++k) fa[k] = vals[k];
+#pragma unroll
+    for (int k = 0; k < S::NB; ++k) fb[k] = vals[S::NA + k];
+    block_reduce_rs_tail<S::NA, S::NB, NW>(fa, fb, lds, out_lds);
+  } else {
+    constexpr int NV = ((NT + 15) / 16) * 16;
+    double flat[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) flat[k] = k < NT ? vals[k] : 0.0;
+    block_reduce_rs<NV, NW>(flat, lds, out_lds);
+  }
 }
 
 // ===========================================================================
@@ -1822,17 +1952,15 @@ void k_back(BackArgs<T> A) {
   }
 
   if constexpr (MODE == BACK_H || MODE == BACK_DIAG) {
-    constexpr int NV = ((VB * NQ + 15) / 16) * 16;
-    __shared__ double lds[kBkWaves * NV];
-    __shared__ double tot[NV];
-    double flat[NV];
-#pragma unroll
-    for (int k = 0; k < NV; ++k) flat[k] = 0.0;
+    constexpr int NT = VB * NQ, NS = RsShape<NT>::NS;
+    __shared__ double lds[kBkWaves * NS];
+    __shared__ double tot[NS];
+    double flat[NT];
 #pragma unroll
     for (int u = 0; u < VB; ++u)
 #pragma unroll
       for (int q = 0; q < NQ; ++q) flat[u * NQ + q] = pq[u][q];
-    block_reduce_rs<NV, kBkWaves>(flat, lds, tot);
+    block_reduce_flat<NT, kBkWaves>(flat, lds, tot);
     const int t = threadIdx.x;
     if (t < VB * NQ && t / NQ < nv) {
       const int P = gridDim.x * gridDim.y;
@@ -2081,17 +2209,15 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
     if (inb2) back_epilogue<T, MH, MODE, NQ, VBR, true>(A, i2, j, rc, v0, nv, r2, pq, mq * MH);
   }
   if constexpr (MODE == BACK_H || MODE == BACK_DIAG) {
-    constexpr int NV = ((MH * NQ + 15) / 16) * 16;
-    __shared__ double lds[kBkWaves * NV];
-    __shared__ double tot[NV];
-    double flat[NV];
-#pragma unroll
-    for (int k = 0; k < NV; ++k) flat[k] = 0.0;
+    constexpr int NT = MH * NQ, NS = RsShape<NT>::NS;
+    __shared__ double lds[kBkWaves * NS];
+    __shared__ double tot[NS];
+    double flat[NT];
 #pragma unroll
     for (int u = 0; u < MH; ++u)
 #pragma unroll
       for (int q = 0; q < NQ; ++q) flat[u * NQ + q] = pq[u][q];
-    block_reduce_rs<NV, kBkWaves>(flat, lds, tot);
+    block_reduce_flat<NT, kBkWaves>(flat, lds, tot);
     const int t = threadIdx.x;
     if (t < MH * NQ && t / NQ < nv) {
       const int P = gridDim.x * gridDim.y;
@@ -2846,6 +2972,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce_rows(const double* __restrict
   block_reduce<1>(a, lds);
   if (threadIdx.x == 0) out[(size_t)(r / G) * ostride + ooff + (r % G)] = a[0];
 }
+
 
 // K x and K^T p for the operator API (float64 node-major)
 __global__ void k_tv_grad(const double* __restrict__ x, double* __restrict__ gx, double* __restrict__ gy, int N) {
