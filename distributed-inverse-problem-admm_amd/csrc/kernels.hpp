@@ -1580,6 +1580,9 @@ constexpr int kBAngC = ADMM_BK_ANGC;  // angles per staged sinogram-window chunk
 #ifndef ADMM_DIAG_G
 #define ADMM_DIAG_G 2
 #endif
+#ifndef ADMM_BK_DMA
+#define ADMM_BK_DMA 1  // mirror back projector (H mode): window bins staged by LDS-DMA
+#endif
 constexpr int kDiagG = ADMM_DIAG_G;  // nodes per staging pass of the DIAG epilogue
 constexpr int kDiagScratch = kDiagG * ((kBTI + 2) * (kBTJ + 2) + 2 * (kBTI + 1) * (kBTJ + 1));
 template <typename T, int VB, int VS = VB>
@@ -2017,8 +2020,19 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
   constexpr int ANGC_DIAG = (98304 / (2 * NPL * kBWin * PB)) & ~3;
   constexpr int ANGC = (MODE == BACK_DIAG && ANGC_ > ANGC_DIAG) ? ANGC_DIAG : ANGC_;
   static_assert(ANGC % 4 == 0 && ANGC >= 4, "angle chunks are read as int4 groups");
-  __shared__ Pack<T, PV> win[2][NPL][ANGC][kBWin];   // [window: upper / mirror tile]
-  __shared__ int4 kmin_s[2][2][ANGC / 4 + 1];         // [buffer][window]: byte offsets koff
+  // DMA (round 6, BACK_H with 16-byte window packs): the window bins go straight from the
+  // sinogram into LDS by LDS-DMA (buffer_load ... lds, no staging VGPRs, no LDS writes by the
+  // waves) into two chunk buffers; the byte offset of a chunk's buffer is folded into its koff,
+  // so the taps' LDS bases stay compile-time constants.  One barrier per chunk instead of two:
+  // the next chunk's DMA is issued before this chunk's taps and the barrier after them waits for
+  // it; the window offsets (kmin_s) and first bins (kst_s) rotate over three slots, written two
+  // chunks ahead.
+  constexpr bool DMA = ADMM_BK_DMA && MODE == BACK_H && NPL == 2 && sizeof(Pack<T, PV>) == 16;
+  constexpr int NWB = DMA ? 4 : 2, NKS = DMA ? 3 : 2;
+  constexpr int BUFB = 2 * NPL * ANGC * kBWin * PB;  // bytes of one chunk's windows
+  __shared__ Pack<T, PV> win[NWB][NPL][ANGC][kBWin];  // [buffer x 2 + window (upper / mirror tile)]
+  __shared__ int4 kmin_s[NKS][2][ANGC / 4 + 1];       // [slot][window]: byte offsets koff
+  __shared__ int kst_s[DMA ? 3 : 1][2][DMA ? ANGC + 1 : 1];  // DMA: [slot][window] first bin - kbias
   T acc1[VB], acc2[VB];
 #pragma unroll
   for (int u = 0; u < VB; ++u) acc1[u] = acc2[u] = T(0);
@@ -2032,18 +2046,24 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
     const BackAngleC& g = A.angc[min(t0 + ((int)threadIdx.x % ANGC), n_ang - 1)];
     return make_double2(g.Bi, g.Bj);
   };
-  auto kmin_store = [&](int buf, double2 bij) {
+  auto kmin_store = [&](int buf, double2 bij, int bo = 0) {  // bo: DMA buffer byte offset
     const int w = (int)threadIdx.x / ANGC;  // threads 0 .. 2 ANGC - 1: (window, angle)
     const double xa = (double)ib - c0, xb = (double)ihi - c0;
     const double x0 = w ? -xb : xa, x1 = w ? -xa : xb;  // the window's row range (x-coordinates)
     auto kf = [&](double xx, int jj) { return fma(xx, bij.x, fma((double)jj - c0, bij.y, Kc)); };
     const double kmn = fmin(fmin(kf(x0, jb), kf(x0, jhi)), fmin(kf(x1, jb), kf(x1, jhi)));
     const int a = (int)threadIdx.x % ANGC;
-    int koff = (a * kBWin - ((int)floor(kmn) - 1)) * PB;
+    const int k0w = (int)floor(kmn) - 1;  // the window's first bin (+ kbias)
+    int koff = (a * kBWin - k0w) * PB;
     if constexpr (FB) koff = (int)((unsigned)koff - kKfHi * (unsigned)PB);  // (kf_split)
+    if constexpr (DMA) {
+      koff = (int)((unsigned)koff + (unsigned)bo);
+      kst_s[buf][min(w, 1)][w < 2 ? a : ANGC] = k0w - kbias;
+    }
     reinterpret_cast<int*>(kmin_s[buf][min(w, 1)])[w < 2 ? a : ANGC] = koff;  // (spare slot)
   };
   auto kmin_chunk = [&](int t0, int buf) { kmin_store(buf, kmin_load(t0)); };
+  auto kmin_chunk_b = [&](int t0, int buf, int bo) { kmin_store(buf, kmin_load(t0), bo); };
   constexpr int NE = 2 * ANGC * kBWin * NPL;  // staged packs per chunk
   constexpr int SPER = (NE + kBkThreads - 1) / kBkThreads;
   Pack<T, PV> wst[SPER];
@@ -2142,25 +2162,28 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
     tap1(std::integral_constant<int, 0>{}, g, fma(xi, g.Bi, inner), koff1, tt, acc1);
     tap1(std::integral_constant<int, 1>{}, g, fma(-xi, g.Bi, inner), koff2, tt, acc2);
   };
-  // register-prefetched chunk pipeline (k_back's PF path)
-  kmin_chunk(0, 0);
-  __syncthreads();
-  wfetch(0, 0);
-  wcommit(0);
-  if (ANGC < n_ang) kmin_chunk(ANGC, 1);
-  __syncthreads();
-  for (int t0 = 0, ci = 0; t0 < n_ang; t0 += ANGC, ++ci) {
-    const int nt = min(ANGC, n_ang - t0);
-    const int kb = ci & 1;
-    const double2 rec2 = kmin_load(min(t0 + 2 * ANGC, n_ang - 1));
-    if (t0 + ANGC < n_ang) wfetch(t0 + ANGC, kb ^ 1);  // in flight during this chunk's taps
+  // one chunk's taps, window offsets from kmin_s[kb]
+  auto chunk_taps = [&](int t0, int nt, int kb) {
     t0c = t0;
     int tt = 0;
-    const BackAngleC* gq = A.angc + t0;  // (records at non-negative immediate offsets of one base)
+    // (records at non-negative immediate offsets of one base, read through the constant address
+    // space: scalar loads even where the LDS-DMA intrinsic hides from the compiler that nothing
+    // writes them -- as generic loads they became vector loads whose vmcnt waits also drained
+    // the next chunk's DMA)
+    using CRec = const __attribute__((address_space(4))) BackAngleC;
+    auto rec = [](CRec* r) {  // field by field (no copy constructor binds an address_space(4) object)
+      BackAngleC g;
+      g.Bi = r->Bi;
+      g.Bj = r->Bj;
+      g.ws = r->ws;
+      g.wc = r->wc;
+      return g;
+    };
+    CRec* gq = (CRec*)(uintptr_t)(A.angc + t0);
     for (; tt + 4 <= nt; tt += 4, gq += 4) {
       BackAngleC g[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) g[u] = gq[u];
+      for (int u = 0; u < 4; ++u) g[u] = rec(gq + u);
       const int4 k1 = kmin_s[kb][0][tt >> 2], k2 = kmin_s[kb][1][tt >> 2];
       tap2(g[0], k1.x, k2.x, tt);
       tap2(g[1], k1.y, k2.y, tt + 1);
@@ -2168,14 +2191,85 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
       tap2(g[3], k1.w, k2.w, tt + 3);
     }
     for (; tt < nt; ++tt) {
-      const BackAngleC g = A.angc[t0 + tt];
+      const BackAngleC g = rec((CRec*)(uintptr_t)A.angc + t0 + tt);
       tap2(g, reinterpret_cast<const int*>(kmin_s[kb][0])[tt], reinterpret_cast<const int*>(kmin_s[kb][1])[tt], tt);
     }
-    if (t0 + ANGC < n_ang) {
-      __syncthreads();  // this chunk's taps are done with win and kmin_s[kb]
-      wcommit(t0 + ANGC);
-      kmin_store(kb, rec2);  // (garbage past the last chunk: never read)
-      __syncthreads();
+  };
+  if constexpr (DMA) {
+    // this wave's NI 64-slot pieces of a chunk (slot = ((window x NPL + plane) x ANGC + angle)
+    // x kBWin + bin, the windows' LDS order): fixed for the kernel, so their bin / angle /
+    // plane / window are formed once
+    constexpr int NI = NE / (64 * kBkWaves);
+    static_assert(NE % (64 * kBkWaves) == 0, "whole 64-slot pieces per wave");
+    const int wvu = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    int pbin[NI], pang[NI], pwin[NI];
+    bool pmir[NI];
+#pragma unroll
+    for (int e = 0; e < NI; ++e) {
+      const int q = (wvu * NI + e) * 64 + lane;
+      pbin[e] = q % kBWin;
+      const int rest = q / kBWin;
+      pang[e] = rest % ANGC;
+      pmir[e] = (rest / ANGC) % NPL;
+      pwin[e] = rest / (ANGC * NPL);
+    }
+    auto dma = [&](int t0, int ks, int bo) {
+      const int nt = min(ANGC, n_ang - t0);
+#pragma unroll
+      for (int e = 0; e < NI; ++e) {
+        const int a = pang[e], t = t0 + a;
+        const int k = kst_s[ks][pwin[e]][a] + pbin[e];
+        const int ray = (pmir[e] ? 2 * n_ang - 1 - t : t) * n_det + k;
+        // bins off the detector (and angles past a short last chunk) are out-of-range offsets:
+        // the hardware writes zeros
+        const unsigned voff = (a < nt && k >= 0 && k < n_det) ? (unsigned)ray * (unsigned)(VBR * sizeof(T)) : 0xFFFFFFFFu;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs_sino,
+            (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(&win[0][0][0][0]) + bo +
+                                                       (wvu * NI + e) * 64 * PB),
+            16, voff, 0, 0, 0);
+      }
+    };
+    kmin_chunk_b(0, 0, 0);
+    if (ANGC < n_ang) kmin_chunk_b(ANGC, 1, BUFB);
+    __syncthreads();
+    dma(0, 0, 0);
+    __syncthreads();  // (its fence waits for this wave's LDS-DMA) chunk 0 staged
+    for (int t0 = 0, ci = 0, ks = 0; t0 < n_ang; t0 += ANGC, ++ci, ks = ks == 2 ? 0 : ks + 1) {
+      const int nt = min(ANGC, n_ang - t0);
+      const double2 rec2 = kmin_load(min(t0 + 2 * ANGC, n_ang - 1));
+      const int ks1 = ks == 2 ? 0 : ks + 1, ks2 = ks1 == 2 ? 0 : ks1 + 1;
+      // the next chunk into the other buffer (last read by the previous chunk's taps, done at
+      // the previous barrier), in flight during this chunk's taps
+      if (t0 + ANGC < n_ang) dma(t0 + ANGC, ks1, (ci & 1) ? 0 : BUFB);
+      chunk_taps(t0, nt, ks);
+      if (t0 + ANGC < n_ang) {
+        // chunk + 2's offsets into the slot chunk - 1 used (its taps and DMA are done); its
+        // buffer is this chunk's (the same parity)
+        if (t0 + 2 * ANGC < n_ang) kmin_store(ks2, rec2, (ci & 1) ? BUFB : 0);
+        __syncthreads();  // next chunk's DMA landed (fence), this chunk's taps done, slot ks2 visible
+      }
+    }
+  } else {
+    // register-prefetched chunk pipeline (k_back's PF path)
+    kmin_chunk(0, 0);
+    __syncthreads();
+    wfetch(0, 0);
+    wcommit(0);
+    if (ANGC < n_ang) kmin_chunk(ANGC, 1);
+    __syncthreads();
+    for (int t0 = 0, ci = 0; t0 < n_ang; t0 += ANGC, ++ci) {
+      const int nt = min(ANGC, n_ang - t0);
+      const int kb = ci & 1;
+      const double2 rec2 = kmin_load(min(t0 + 2 * ANGC, n_ang - 1));
+      if (t0 + ANGC < n_ang) wfetch(t0 + ANGC, kb ^ 1);  // in flight during this chunk's taps
+      chunk_taps(t0, nt, kb);
+      if (t0 + ANGC < n_ang) {
+        __syncthreads();  // this chunk's taps are done with win and kmin_s[kb]
+        wcommit(t0 + ANGC);
+        kmin_store(kb, rec2);  // (garbage past the last chunk: never read)
+        __syncthreads();
+      }
     }
   }
   if constexpr (std::is_same<T, float>::value) {
