@@ -143,6 +143,7 @@ struct admm_ctx {
   // mirror mode (kernels.hpp k_fwdg MIRROR): the bound batch projects virtual images over the
   // first half of the angles with the half geometry's context `half` (tables and plans)
   bool mm = false;
+  bool bk_reg = false;  // ADMM_BK_STAGING=reg at creation: register-staged back windows (A/B, tests)
   admm_ctx* half = nullptr;
   Buf xs, xsT, p, pT, Hp, sino, bI, fpart, r, c, d2, e2;
   Buf dsumS;  // D = sum_j q_ij as interleaved samples (BACK_H epilogue)
@@ -487,7 +488,12 @@ int launch_back(admm_ctx* C, BackArgs<T> a, int V, hipStream_t s) {
       a.V = V;
       const int N = C->g.N, Nh = (N + 1) / 2;
       dim3 grid((N + kBTJ - 1) / kBTJ, (Nh + kBTI - 1) / kBTI, ((V + VB - 1) / VB) * (VB / MH));
-      hipLaunchKernelGGL((k_back_mirror<T, VBV, VB, MODE>), grid, dim3(kBkThreads), 0, s, a);
+      bool reg = false;  // the register-staged windows (ADMM_BK_STAGING=reg): where DMA is the default
+      if constexpr (back_mirror_dma<T, VBV, MODE>()) {
+        reg = C->bk_reg;
+        if (reg) hipLaunchKernelGGL((k_back_mirror_reg<T, VBV, VB, MODE>), grid, dim3(kBkThreads), 0, s, a);
+      }
+      if (!reg) hipLaunchKernelGGL((k_back_mirror<T, VBV, VB, MODE>), grid, dim3(kBkThreads), 0, s, a);
       CHECK_LAUNCH();
       return ADMM_OK;
     }
@@ -921,6 +927,10 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
   C->g = g;
   C->dtype = dtype;
   C->device = device;
+  {
+    const char* st = getenv("ADMM_BK_STAGING");
+    C->bk_reg = st && std::string(st) == "reg";
+  }
   C->max_images = max_images;
   C->npix = (int)npix;
   C->mrays = (int)m;

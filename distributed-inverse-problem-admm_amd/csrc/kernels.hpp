@@ -1986,8 +1986,15 @@ void k_back(BackArgs<T> A) {
 // real vector).  Two LDS windows per angle (upper tile, mirror tile) at half the angles per
 // chunk keep the LDS size and the staged bytes per tap of k_back.
 // ===========================================================================
-template <typename T, int VB, int VBR, int MODE>
-__global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
+// the mirror back projector of (T, VB, MODE) stages its windows by LDS-DMA (H mode, 16-byte
+// window packs) unless instantiated with DMAQ = false (the register-staged windows: A/B and the
+// bitwise test, ADMM_BK_STAGING=reg at context creation)
+template <typename T, int VB, int MODE>
+constexpr bool back_mirror_dma() {
+  return ADMM_BK_DMA && MODE == BACK_H && Planes<T, VB>::NPL == 2 && sizeof(Pack<T, Planes<T, VB>::PV>) == 16;
+}
+template <typename T, int VB, int VBR, int MODE, bool DMAQ>
+__device__ __forceinline__ void back_mirror_body(const BackArgs<T>& A) {
   static_assert(MODE == BACK_H || MODE == BACK_INIT || MODE == BACK_DIAG || MODE == BACK_ATB, "batch modes");
   constexpr int MH = VB / 2, MS = VBR / MH;
   static_assert(VB % 2 == 0 && VBR % MH == 0, "mirror: VB = 2 x (a divisor of VBR)");
@@ -2027,7 +2034,7 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
   // the next chunk's DMA is issued before this chunk's taps and the barrier after them waits for
   // it; the window offsets (kmin_s) and first bins (kst_s) rotate over three slots, written two
   // chunks ahead.
-  constexpr bool DMA = ADMM_BK_DMA && MODE == BACK_H && NPL == 2 && sizeof(Pack<T, PV>) == 16;
+  constexpr bool DMA = DMAQ && back_mirror_dma<T, VB, MODE>();
   constexpr int NWB = DMA ? 4 : 2, NKS = DMA ? 3 : 2;
   constexpr int BUFB = 2 * NPL * ANGC * kBWin * PB;  // bytes of one chunk's windows
   __shared__ Pack<T, PV> win[NWB][NPL][ANGC][kBWin];  // [buffer x 2 + window (upper / mirror tile)]
@@ -2319,6 +2326,17 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
       A.part[((size_t)v0 * NQ + t) * P + b] = tot[t];
     }
   }
+}
+
+// the kernels: windows by LDS-DMA where back_mirror_dma (the default), register-staged
+// (k_back_mirror_reg, ADMM_BK_STAGING=reg at context creation; the same results bit for bit)
+template <typename T, int VB, int VBR, int MODE>
+__global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
+  back_mirror_body<T, VB, VBR, MODE, true>(A);
+}
+template <typename T, int VB, int VBR, int MODE>
+__global__ __launch_bounds__(kBkThreads) void k_back_mirror_reg(BackArgs<T> A) {
+  back_mirror_body<T, VB, VBR, MODE, false>(A);
 }
 
 // ===========================================================================

@@ -113,3 +113,24 @@ def test_default_mode_by_sample_type(cuda, monkeypatch):
         _, Q = make_precisions(ops)
         nb = NodeBatch(ops[0].geom, dtype, plan, sinos, Q, 2.0, 0.02, 0.2, 3, 3, "iso", ph, 0)
         assert nb.mirror == want and nb.ctx_vb == vb, (dtype, V, a, nb.mirror, nb.ctx_vb)
+
+
+@pytest.mark.parametrize("dtype,V,N", [("float32", 5, 64), ("float32", 16, 128), ("float32", 4, 47),
+                                       ("float64", 2, 48)])
+def test_back_windows_by_lds_dma_bitwise(cuda, monkeypatch, dtype, V, N):
+    """The mirror back projector's H mode stages its sinogram windows by LDS-DMA into two
+    chunk buffers (kernels.hpp k_back_mirror, DMA); ADMM_BK_STAGING=reg at context creation
+    selects the register-staged windows.  The same bins land in LDS and the taps read them in
+    the same order: whole trajectories bitwise equal (5 nodes = a full and a one-node lane
+    block; 16 nodes = four lane blocks, two tiles per CU at 512^2 in the bench; odd N)."""
+    monkeypatch.setenv("ADMM_FWD_MIRROR", "1")
+    runs = []
+    for staging in ("dma", "reg"):
+        monkeypatch.setenv("ADMM_BK_STAGING", staging)
+        _, _, _, _, _, x, h = _run(N, V, 24, dtype)
+        runs.append((x, {k: np.asarray(h[k]) for k in ("primal", "dual", "obj_total", "mse_sino_total",
+                                                       "g_norm_history")}))
+    (x0, h0), (x1, h1) = runs
+    assert np.array_equal(x0, x1), float(np.max(np.abs(x0 - x1)))
+    for k in h0:
+        assert np.array_equal(h0[k], h1[k]), k
