@@ -92,3 +92,25 @@ def test_two_ranks_on_one_gpu_match_one_rank_bitwise(cuda, graph, fusion, angles
         assert np.array_equal(x1, x2), (graph, fusion, r)
         for k in h1:
             assert np.array_equal(h1[k], h2[k]), (k, graph, fusion)
+
+
+@pytest.mark.timeout(180)
+def test_rccl_calls_on_one_rank(cuda):
+    """The RCCL calls of the multi-GPU path on a one-rank "nccl" group (scripts/probes/
+    rccl_one_gpu.py, its own process): all_gather_into_tensor of float64 device rows (async),
+    a grouped batch_isend_irecv into a row slice (to the rank itself), all_reduce SUM / MAX of
+    float64 and int64 device tensors, barrier.  RCCL refuses two ranks on one GPU, so the
+    cross-rank semantics are covered by the gloo tests; this pins the call signatures, dtypes and
+    views on RCCL itself."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = socket.socket()
+    port.bind(("127.0.0.1", 0))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port.getsockname()[1]))
+    port.close()
+    p = subprocess.run([sys.executable, os.path.join(root, "scripts", "probes", "rccl_one_gpu.py")],
+                       env=env, capture_output=True, text=True, timeout=150)
+    print(p.stdout[-400:])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "'all_gather_into_tensor': True" in p.stdout and "'batch_isend_irecv_self': True" in p.stdout
