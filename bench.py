@@ -522,14 +522,25 @@ def launch_ranks(n: int) -> int:
     return status
 
 
+def back_kernel_name(tr, tname, vb, mirror):
+    """The batch's in-solve back projector (BACK_H = mode 3) as rocprofv3 names it: in mirror mode
+    k_back_mirror_2<T, VBV, VBR> (two lane blocks per block, where the grid fills the chip) or
+    k_back_mirror<T, VBV, VBR, 3>; k_back<T, VB, 3, false> otherwise.  With a traffic file, the
+    one of the mirror pair that ran."""
+    vbv = min(2 * vb, 32 // (8 if tname == "double" else 4))
+    if not mirror:
+        return f"admm::k_back<{tname}, {vb}, 3, false>"
+    two = f"admm::k_back_mirror_2<{tname}, {vbv}, {vb}>"
+    if tr and two in tr.get("kernels", {}):
+        return two
+    return f"admm::k_back_mirror<{tname}, {vbv}, {vb}, 3>"
+
+
 def back_kernel_traffic(tr, tname, vb, mirror):
-    """PMC bytes per launch of the batch's in-solve back projector (BACK_H = mode 3):
-    k_back_mirror<T, VBV, VBR, 3> in mirror mode, k_back<T, VB, 3, false> otherwise."""
+    """PMC bytes per launch of the batch's in-solve back projector (back_kernel_name)."""
     if not tr:
         return None
-    vbv = min(2 * vb, 32 // (8 if tname == "double" else 4))
-    want = f"admm::k_back_mirror<{tname}, {vbv}, {vb}, 3>" if mirror else f"admm::k_back<{tname}, {vb}, 3, false>"
-    return tr["kernels"].get(want, {}).get("hbm_bytes_per_launch")
+    return tr["kernels"].get(back_kernel_name(tr, tname, vb, mirror), {}).get("hbm_bytes_per_launch")
 
 
 def _roof(kernel, traffic, tr_file, ms, compulsory, lds_bytes, extra=None, stale=None):
@@ -615,8 +626,10 @@ def projector_rooflines(r, workload, fwd_reps):
     # back projector in H mode (A^T s fused with H p = A^T A p + rho D p + mu K^T K p and the five
     # CG dot products): compulsory = sinogram, p, D (samples) and r (float64) read once, Hp written
     back_comp = V * m * sb + 3 * V * n * sb + V * n * 8
-    back = _roof((f"k_back_mirror<{tname},{vbv},{vb},BACK_H> (mirror mode: pixel pairs (i, j), (N-1-i, j) "
-                  f"of the upper half over half the angles; " if mirror else f"k_back<{tname},{vb},BACK_H> (")
+    bname = back_kernel_name(tr, tname, vb, mirror).replace("admm::", "").replace(" ", "")
+    back = _roof((f"{bname} (BACK_H; mirror mode: pixel pairs (i, j), (N-1-i, j) of the upper half over half "
+                  f"the angles{'; two lane blocks per block' if 'mirror_2' in bname else ''}; " if mirror
+                  else f"{bname} (BACK_H; ")
                  + f"pixel-driven Joseph adjoint taps from LDS sinogram windows, fused H epilogue and CG "
                  f"dot partials; {chunks})",
                  back_kernel_traffic(tr, tname, vb, mirror), tr_file, back_ms, back_comp,

@@ -143,7 +143,11 @@ struct admm_ctx {
   // mirror mode (kernels.hpp k_fwdg MIRROR): the bound batch projects virtual images over the
   // first half of the angles with the half geometry's context `half` (tables and plans)
   bool mm = false;
-  bool bk_reg = false;  // ADMM_BK_STAGING=reg at creation: register-staged back windows (A/B, tests)
+  // ADMM_BK_STAGING at creation (A/B, tests): "reg" register-staged back windows, "dma1" LDS-DMA
+  // windows with one lane block per block, "dma2" two lane blocks per block wherever the lane
+  // blocks pair up; default: LDS-DMA, two lane blocks per block where the grid still fills the chip
+  int bk_staging = 0;   // 0 default, 1 reg, 2 dma1, 3 dma2
+  int n_cu = 0;         // compute units of the device
   admm_ctx* half = nullptr;
   Buf xs, xsT, p, pT, Hp, sino, bI, fpart, r, c, d2, e2;
   Buf dsumS;  // D = sum_j q_ij as interleaved samples (BACK_H epilogue)
@@ -488,12 +492,22 @@ int launch_back(admm_ctx* C, BackArgs<T> a, int V, hipStream_t s) {
       a.V = V;
       const int N = C->g.N, Nh = (N + 1) / 2;
       dim3 grid((N + kBTJ - 1) / kBTJ, (Nh + kBTI - 1) / kBTI, ((V + VB - 1) / VB) * (VB / MH));
-      bool reg = false;  // the register-staged windows (ADMM_BK_STAGING=reg): where DMA is the default
+      bool done = false;
       if constexpr (back_mirror_dma<T, VBV, MODE>()) {
-        reg = C->bk_reg;
-        if (reg) hipLaunchKernelGGL((k_back_mirror_reg<T, VBV, VB, MODE>), grid, dim3(kBkThreads), 0, s, a);
+        if (C->bk_staging == 1) {  // the register-staged windows (where DMA is the default)
+          hipLaunchKernelGGL((k_back_mirror_reg<T, VBV, VB, MODE>), grid, dim3(kBkThreads), 0, s, a);
+          done = true;
+        } else if constexpr (std::is_same<T, float>::value && ADMM_BK_LB2) {
+          // two lane blocks per block while half the blocks still give every CU one
+          const bool fills = (long)grid.x * grid.y * grid.z >= 2L * C->n_cu;
+          if (grid.z % 2 == 0 && (C->bk_staging == 3 || (C->bk_staging == 0 && fills))) {
+            hipLaunchKernelGGL((k_back_mirror_2<T, VBV, VB>), dim3(grid.x, grid.y, grid.z / 2), dim3(kBkThreads), 0,
+                               s, a);
+            done = true;
+          }
+        }
       }
-      if (!reg) hipLaunchKernelGGL((k_back_mirror<T, VBV, VB, MODE>), grid, dim3(kBkThreads), 0, s, a);
+      if (!done) hipLaunchKernelGGL((k_back_mirror<T, VBV, VB, MODE>), grid, dim3(kBkThreads), 0, s, a);
       CHECK_LAUNCH();
       return ADMM_OK;
     }
@@ -929,8 +943,10 @@ int admm_ctx_create(admm_ctx** out, const admm_geom* geom, int dtype, int max_im
   C->device = device;
   {
     const char* st = getenv("ADMM_BK_STAGING");
-    C->bk_reg = st && std::string(st) == "reg";
+    const std::string v = st ? st : "";
+    C->bk_staging = v == "reg" ? 1 : v == "dma1" ? 2 : v == "dma2" ? 3 : 0;
   }
+  HIPCHK(hipDeviceGetAttribute(&C->n_cu, hipDeviceAttributeMultiprocessorCount, device));
   C->max_images = max_images;
   C->npix = (int)npix;
   C->mrays = (int)m;

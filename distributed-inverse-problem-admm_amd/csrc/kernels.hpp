@@ -1583,6 +1583,9 @@ constexpr int kBAngC = ADMM_BK_ANGC;  // angles per staged sinogram-window chunk
 #ifndef ADMM_BK_DMA
 #define ADMM_BK_DMA 1  // mirror back projector (H mode): window bins staged by LDS-DMA
 #endif
+#ifndef ADMM_BK_LB2
+#define ADMM_BK_LB2 1  // ... and two lane blocks per block where the grid still fills the chip
+#endif
 constexpr int kDiagG = ADMM_DIAG_G;  // nodes per staging pass of the DIAG epilogue
 constexpr int kDiagScratch = kDiagG * ((kBTI + 2) * (kBTJ + 2) + 2 * (kBTI + 1) * (kBTJ + 1));
 template <typename T, int VB, int VS = VB>
@@ -2337,6 +2340,213 @@ __global__ __launch_bounds__(kBkThreads) void k_back_mirror(BackArgs<T> A) {
 template <typename T, int VB, int VBR, int MODE>
 __global__ __launch_bounds__(kBkThreads) void k_back_mirror_reg(BackArgs<T> A) {
   back_mirror_body<T, VB, VBR, MODE, false>(A);
+}
+
+// ===========================================================================
+// Mirror back projector, H mode, two lane blocks per block (round 6, `ADMM_BK_LB2`): the same
+// pixel tile of lane blocks 2z and 2z + 1 (8 real nodes).  A tap's position, weights and LDS
+// address are formed once and applied to both lane blocks' windows (the per-tap overhead of
+// k_back_mirror is paid per 8 nodes instead of 4), the windows arrive by LDS-DMA as in
+// k_back_mirror's DMA path (half the angles per chunk: the two lane blocks' windows in two
+// buffers fill the same 98 KB), and the grid is half as many blocks.  Per lane block the
+// arithmetic is k_back_mirror's in the same order: bitwise the same Hp and dot partials.
+// ===========================================================================
+template <typename T, int VB, int VBR>
+__global__ __launch_bounds__(kBkThreads) void k_back_mirror_2(BackArgs<T> A) {
+  constexpr int MODE = BACK_H, NQ = 5, LB = 2;
+  constexpr int MH = VB / 2, MS = VBR / MH;
+  static_assert(VB % 2 == 0 && VBR % MH == 0, "mirror: VB = 2 x (a divisor of VBR)");
+  constexpr int NPL = Planes<T, VB>::NPL, PV = Planes<T, VB>::PV;
+  constexpr int PB = (int)sizeof(Pack<T, PV>);
+  static_assert(std::is_same<T, float>::value && NPL == 2 && PB == 16, "float32 16-byte window packs");
+  const int N = A.N, n_det = A.n_det, n_ang = A.n_ang;  // n_ang: the half geometry's a/2 angles
+  const int Nh = (N + 1) / 2;
+  const size_t m_full = (size_t)2 * n_ang * n_det;
+  const int jb = blockIdx.x * kBTJ, ib = blockIdx.y * kBTI;  // upper tile: rows ib .. (< Nh)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int j = jb + 16 * (wv % kBkPatchJ) + (lane & 15);
+  const int i = ib + 4 * (wv / kBkPatchJ) + (lane >> 4);
+  const int i2 = N - 1 - i;                  // the mirror pixel's row
+  const bool inb = (i < Nh) && (j < N);
+  const bool inb2 = inb && (i2 != i);        // (odd N: the middle row pairs with itself)
+  const double c0 = 0.5 * (N - 1);
+  const double xi = (double)min(i, Nh - 1) - c0, yj = (double)min(j, N - 1) - c0;
+  const int jhi = min(jb + kBTJ - 1, N - 1), ihi = min(ib + kBTI - 1, Nh - 1);
+  const int kbias = A.kbias;
+  const double Kc = A.K + (double)kbias;
+  const double Kcb = Kc + kKfBias;  // (kf_split)
+  constexpr int ANGC = kBAngC / 4;  // half of k_back_mirror's: two lane blocks' windows per buffer
+  static_assert(ANGC % 4 == 0 && ANGC >= 4, "angle chunks are read as int4 groups");
+  constexpr int WINB = 2 * NPL * ANGC * kBWin * PB;  // bytes of one lane block's windows per chunk
+  constexpr int BUFB = LB * WINB;                    // bytes of one chunk buffer
+  __shared__ Pack<T, PV> win[2 * LB * 2][NPL][ANGC][kBWin];  // [buffer][lane block][window]
+  __shared__ int4 kmin_s[3][2][ANGC / 4 + 1];                // [slot][window]: byte offsets koff
+  __shared__ int kst_s[3][2][ANGC + 1];                      // [slot][window]: first bin - kbias
+  T acc1[LB][VB], acc2[LB][VB];
+#pragma unroll
+  for (int l = 0; l < LB; ++l)
+#pragma unroll
+    for (int u = 0; u < VB; ++u) acc1[l][u] = acc2[l][u] = T(0);
+
+  auto kmin_load = [&](int t0) {
+    const BackAngleC& g = A.angc[min(t0 + ((int)threadIdx.x % ANGC), n_ang - 1)];
+    return make_double2(g.Bi, g.Bj);
+  };
+  auto kmin_store = [&](int ks, double2 bij, int bo) {  // bo: the chunk buffer's byte offset
+    const int w = (int)threadIdx.x / ANGC;  // threads 0 .. 2 ANGC - 1: (window, angle)
+    const double xa = (double)ib - c0, xb = (double)ihi - c0;
+    const double x0 = w ? -xb : xa, x1 = w ? -xa : xb;  // the window's row range (x-coordinates)
+    auto kf = [&](double xx, int jj) { return fma(xx, bij.x, fma((double)jj - c0, bij.y, Kc)); };
+    const double kmn = fmin(fmin(kf(x0, jb), kf(x0, jhi)), fmin(kf(x1, jb), kf(x1, jhi)));
+    const int a = (int)threadIdx.x % ANGC;
+    const int k0w = (int)floor(kmn) - 1;  // the window's first bin (+ kbias)
+    const int koff = (int)((unsigned)((a * kBWin - k0w) * PB) - kKfHi * (unsigned)PB + (unsigned)bo);
+    kst_s[ks][min(w, 1)][w < 2 ? a : ANGC] = k0w - kbias;                      // (spare slot)
+    reinterpret_cast<int*>(kmin_s[ks][min(w, 1)])[w < 2 ? a : ANGC] = koff;
+  };
+  constexpr int NE = LB * 2 * ANGC * kBWin * NPL;  // staged packs per chunk
+  constexpr int NI = NE / (64 * kBkWaves);         // 64-slot pieces per wave
+  static_assert(NE % (64 * kBkWaves) == 0 && (ANGC * kBWin) % 64 == 0, "whole pieces, one (lane block, window, plane) each");
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
+  auto dma = [&](int t0, int ks, int bo) {
+    const int nt = min(ANGC, n_ang - t0);
+#pragma unroll
+    for (int e = 0; e < NI; ++e) {
+      // slot q = (((lane block x 2 + window) x NPL + plane) x ANGC + angle) x kBWin + bin
+      const int q0 = (wvu * NI + e) * 64;  // a piece lies in one (lane block, window, plane)
+      const int q = q0 + lane;
+      const int bin = q % kBWin, a = (q / kBWin) % ANGC;
+      const int lwp = q0 / (ANGC * kBWin), pl = lwp % NPL, w = (lwp / NPL) % 2, l = lwp / (2 * NPL);
+      const int z = (int)blockIdx.z * LB + l;
+      const T* base = A.sino + (size_t)(z / MS) * m_full * VBR + (z % MS) * MH;  // lane block l
+      const uint64_t b = (uint64_t)(uintptr_t)base;
+      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+      const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+      const __amdgpu_buffer_rsrc_t rs =
+          make_rsrc((const void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (uint32_t)(m_full * VBR * sizeof(T)));
+      const int t = t0 + a;
+      const int k = kst_s[ks][w][a] + bin;
+      const int ray = (pl ? 2 * n_ang - 1 - t : t) * n_det + k;
+      const unsigned voff = (a < nt && k >= 0 && k < n_det) ? (unsigned)ray * (unsigned)(VBR * sizeof(T)) : 0xFFFFFFFFu;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(&win[0][0][0][0]) + bo + q0 * PB), 16,
+          voff, 0, 0, 0);
+    }
+  };
+  // one angle's taps of one pixel from window W of both lane blocks: the weights and the LDS
+  // address once (k_back_mirror's tap1), the two lane blocks' samples at the same offset
+  auto tap1 = [&](auto wc_, const BackAngleC& g, double kf, int koff, T(&acc)[LB][VB]) {
+    constexpr int w = decltype(wc_)::value;
+    unsigned hi;
+    float2v wc, fv, ww;
+    float fu;
+    kf_split(kf, hi, fu);
+    fv.x = fu;
+    asm("v_mov_b64 %0, %1" : "=v"(wc) : "s"(g.wc));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] clamp" : "=v"(ww) : "v"(fv), "s"(g.ws), "v"(wc));
+    const T w0 = ww.x, w1 = ww.y;
+    const int off = kf_addr<PB>(hi, koff);  // (koff carries -kKfHi x PB and the buffer offset)
+#pragma unroll
+    for (int l = 0; l < LB; ++l)
+#pragma unroll
+      for (int q = 0; q < NPL; ++q) {
+        const char* wb = reinterpret_cast<const char*>(&win[l * 2 + w][q][0][0]) + off;
+        const Pack<T, PV> s0 = *reinterpret_cast<const Pack<T, PV>*>(wb);
+        const Pack<T, PV> s1 = *reinterpret_cast<const Pack<T, PV>*>(wb + PB);
+#pragma unroll
+        for (int e = 0; e < PV; ++e) {
+          acc[l][q * PV + e] = fma(w0, s0.v[e], acc[l][q * PV + e]);
+          acc[l][q * PV + e] = fma(w1, s1.v[e], acc[l][q * PV + e]);
+        }
+      }
+  };
+  auto tap2 = [&](const BackAngleC& g, int koff1, int koff2) {
+    const double inner = fma(yj, g.Bj, Kcb);
+    tap1(std::integral_constant<int, 0>{}, g, fma(xi, g.Bi, inner), koff1, acc1);
+    tap1(std::integral_constant<int, 1>{}, g, fma(-xi, g.Bi, inner), koff2, acc2);
+  };
+  using CRec = const __attribute__((address_space(4))) BackAngleC;
+  auto rec = [](CRec* r) {  // field by field (no copy constructor binds an address_space(4) object)
+    BackAngleC g;
+    g.Bi = r->Bi;
+    g.Bj = r->Bj;
+    g.ws = r->ws;
+    g.wc = r->wc;
+    return g;
+  };
+  auto chunk_taps = [&](int t0, int nt, int ks) {
+    int tt = 0;
+    CRec* gq = (CRec*)(uintptr_t)(A.angc + t0);
+    for (; tt + 4 <= nt; tt += 4, gq += 4) {
+      BackAngleC g[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) g[u] = rec(gq + u);
+      const int4 k1 = kmin_s[ks][0][tt >> 2], k2 = kmin_s[ks][1][tt >> 2];
+      tap2(g[0], k1.x, k2.x);
+      tap2(g[1], k1.y, k2.y);
+      tap2(g[2], k1.z, k2.z);
+      tap2(g[3], k1.w, k2.w);
+    }
+    for (; tt < nt; ++tt)
+      tap2(rec(gq + (tt & 3)), reinterpret_cast<const int*>(kmin_s[ks][0])[tt],
+           reinterpret_cast<const int*>(kmin_s[ks][1])[tt]);
+  };
+  kmin_store(0, kmin_load(0), 0);
+  if (ANGC < n_ang) kmin_store(1, kmin_load(ANGC), BUFB);
+  __syncthreads();
+  dma(0, 0, 0);
+  __syncthreads();  // (its fence waits for this wave's LDS-DMA) chunk 0 staged
+  for (int t0 = 0, ci = 0, ks = 0; t0 < n_ang; t0 += ANGC, ++ci, ks = ks == 2 ? 0 : ks + 1) {
+    const int nt = min(ANGC, n_ang - t0);
+    const double2 rec2 = kmin_load(min(t0 + 2 * ANGC, n_ang - 1));
+    const int ks1 = ks == 2 ? 0 : ks + 1, ks2 = ks1 == 2 ? 0 : ks1 + 1;
+    if (t0 + ANGC < n_ang) dma(t0 + ANGC, ks1, (ci & 1) ? 0 : BUFB);
+    chunk_taps(t0, nt, ks);
+    if (t0 + ANGC < n_ang) {
+      if (t0 + 2 * ANGC < n_ang) kmin_store(ks2, rec2, (ci & 1) ? BUFB : 0);
+      __syncthreads();  // next chunk's DMA landed (fence), this chunk's taps done, slot ks2 visible
+    }
+  }
+  // per lane block: k_back_mirror's epilogue (the real A^T s of both pixels, the fused H epilogue
+  // and the block's 20 dot partials through the same reduction), one lane block at a time
+  constexpr int NT = MH * NQ, NS = RsShape<NT>::NS;
+  __shared__ double lds[kBkWaves * NS];
+  __shared__ double tot[NS];
+  const int P = gridDim.x * gridDim.y;
+  const int b = blockIdx.y * gridDim.x + blockIdx.x;
+#pragma unroll
+  for (int l = 0; l < LB; ++l) {
+    if (A.wexp != 0) {
+#pragma unroll
+      for (int u = 0; u < VB; ++u) {
+        acc1[l][u] = ldexpf(acc1[l][u], A.wexp);
+        acc2[l][u] = ldexpf(acc2[l][u], A.wexp);
+      }
+    }
+    T r1[MH], r2[MH];
+#pragma unroll
+    for (int h = 0; h < MH; ++h) {
+      r1[h] = acc1[l][h] + acc2[l][MH + h];
+      r2[h] = acc2[l][h] + acc1[l][MH + h];
+    }
+    double pq[MH][NQ];
+#pragma unroll
+    for (int u = 0; u < MH; ++u)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) pq[u][q] = 0.0;
+    const int z = (int)blockIdx.z * LB + l, rc = z / MS, mq = z % MS;
+    const int v0 = rc * VBR + mq * MH, nv = min(MH, A.V - v0);
+    if (inb) back_epilogue<T, MH, MODE, NQ, VBR>(A, i, j, rc, v0, nv, r1, pq, mq * MH);
+    if (inb2) back_epilogue<T, MH, MODE, NQ, VBR, true>(A, i2, j, rc, v0, nv, r2, pq, mq * MH);
+    double flat[NT];
+#pragma unroll
+    for (int u = 0; u < MH; ++u)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) flat[u * NQ + q] = pq[u][q];
+    block_reduce_flat<NT, kBkWaves>(flat, lds, tot);
+    const int t = threadIdx.x;
+    if (t < NT && t / NQ < nv) A.part[((size_t)v0 * NQ + t) * P + b] = tot[t];
+  }
 }
 
 // ===========================================================================

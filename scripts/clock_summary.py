@@ -7,7 +7,7 @@ import glob
 import sys
 
 d = sys.argv[1]
-pats = sys.argv[2:] or ["k_fwdg<float, 8", "k_back_mirror<float, 8, 4, 3>", "k_cg_update", "k_tv_update"]
+pats = sys.argv[2:] or ["k_fwdg<float, 8", "k_back_mirror_2<float, 8, 4>", "k_back_mirror<float, 8, 4, 3>", "k_cg_update", "k_tv_update"]
 f = glob.glob(f"{d}/**/*counter_collection.csv", recursive=True) + glob.glob(f"{d}/*counter_collection.csv")
 acc = collections.defaultdict(lambda: [0, 0.0, 0.0])
 for r in csv.DictReader(open(f[0])):

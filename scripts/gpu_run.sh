@@ -37,10 +37,10 @@ for step in "$@"; do
       python scripts/pmc_summary.py ${step}_${TAG} "k_fwdg<" "k_back" ;;
     sq5)  # SQ counters (scripts/passes_sq_r5.txt: issue, LDS, wait, f64 / cvt counts) of the C3 headline, default modes
       PASSFILE=scripts/passes_sq_r5.txt run sq5 600 bash scripts/pmc.sh sq5_${TAG} > gpurun_out/sq5_${TAG}.log 2>&1 || { tail -5 gpurun_out/sq5_${TAG}.log; exit 1; }
-      python scripts/pmc_summary.py sq5_${TAG} "k_fwdg<" "k_back_mirror<float, 8, 4, 3>" "k_tv_update<float, 4, false, true, true, true>" "k_cg_update<float, 4, true, false>" | tee gpurun_out/sq5_${TAG}_summary.txt ;;
+      python scripts/pmc_summary.py sq5_${TAG} "k_fwdg<" "k_back_mirror_2<float, 8, 4>" "k_back_mirror<float, 8, 4, 3>" "k_tv_update<float, 4, false, true, true, true>" "k_cg_update<float, 4, true, false>" | tee gpurun_out/sq5_${TAG}_summary.txt ;;
     tvc)  # round 6: TA / TCP / TCC / TD / SQ counters of the TV and CG updates (scripts/passes_tv_r6.txt)
       PASS_TIMEOUT=150 PASSFILE=scripts/passes_tv_r6.txt run tvc 700 bash scripts/pmc.sh tvc_${TAG} > gpurun_out/tvc_${TAG}.log 2>&1 || { tail -5 gpurun_out/tvc_${TAG}.log; exit 1; }
-      python scripts/pmc_summary.py tvc_${TAG} "k_tv_update<float, 4, false, true, true, true>" "k_cg_update<float, 4, true, false>" "k_back_mirror<float, 8, 4, 3>" | tee gpurun_out/tvc_${TAG}_summary.txt ;;
+      python scripts/pmc_summary.py tvc_${TAG} "k_tv_update<float, 4, false, true, true, true>" "k_cg_update<float, 4, true, false>" "k_back_mirror_2<float, 8, 4>" | tee gpurun_out/tvc_${TAG}_summary.txt ;;
     tests=*)
       expr=${step#tests=}
       if [ "$expr" = all ]; then k=(); else k=(-k "$expr"); fi

@@ -119,18 +119,21 @@ def test_default_mode_by_sample_type(cuda, monkeypatch):
                                        ("float64", 2, 48)])
 def test_back_windows_by_lds_dma_bitwise(cuda, monkeypatch, dtype, V, N):
     """The mirror back projector's H mode stages its sinogram windows by LDS-DMA into two
-    chunk buffers (kernels.hpp k_back_mirror, DMA); ADMM_BK_STAGING=reg at context creation
-    selects the register-staged windows.  The same bins land in LDS and the taps read them in
-    the same order: whole trajectories bitwise equal (5 nodes = a full and a one-node lane
-    block; 16 nodes = four lane blocks, two tiles per CU at 512^2 in the bench; odd N)."""
+    chunk buffers (kernels.hpp k_back_mirror, DMA), and where the grid fills the chip runs two
+    lane blocks per block (k_back_mirror_2); ADMM_BK_STAGING at context creation selects
+    "dma1" (one lane block per block), "reg" (register-staged windows) or "dma2" (two lane
+    blocks wherever they pair up).  The same bins land in LDS and every lane block's taps read
+    them in the same order: whole trajectories bitwise equal (5 nodes = a full and a one-node
+    lane block; 16 nodes = four lane blocks; odd N; float64 keeps one lane block)."""
     monkeypatch.setenv("ADMM_FWD_MIRROR", "1")
     runs = []
-    for staging in ("dma", "reg"):
+    for staging in ("dma1", "reg", "dma2"):
         monkeypatch.setenv("ADMM_BK_STAGING", staging)
         _, _, _, _, _, x, h = _run(N, V, 24, dtype)
         runs.append((x, {k: np.asarray(h[k]) for k in ("primal", "dual", "obj_total", "mse_sino_total",
                                                        "g_norm_history")}))
-    (x0, h0), (x1, h1) = runs
-    assert np.array_equal(x0, x1), float(np.max(np.abs(x0 - x1)))
-    for k in h0:
-        assert np.array_equal(h0[k], h1[k]), k
+    (x0, h0) = runs[0]
+    for x1, h1 in runs[1:]:
+        assert np.array_equal(x0, x1), float(np.max(np.abs(x0 - x1)))
+        for k in h0:
+            assert np.array_equal(h0[k], h1[k]), k
