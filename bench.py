@@ -243,14 +243,22 @@ def cpu_baseline(N, a, b, q, x_gpu, procs=None, budget=CPU_BASELINE_SECONDS):
 TRAFFIC_FILES = {"C3": "profiles/r6_traffic.json", "weak8": "profiles/r6_traffic_weak8.json"}
 
 
+def fwd_kernel_name(tr, tname, vb, mirror):
+    """The batch's forward projector instantiation as rocprofv3 names it: k_fwdg<T, VB, MIRROR,
+    VBR, CPB> (mirror mode projects virtual width 2 x VBR; CPB = 2 virtual chunks per block where
+    the halved block table fills the chip); with a traffic file, the one that ran."""
+    head = f"admm::k_fwdg<{tname}, {min(2 * vb, 32 // (8 if tname == 'double' else 4)) if mirror else vb}, " \
+           f"{'true' if mirror else 'false'}, {vb}"
+    names = [f"{head}, 2>", f"{head}, 1>", f"{head}>"]
+    kern = (tr or {}).get("kernels", {})
+    return next((n for n in names if n in kern), names[1])
+
+
 def fwd_kernel_traffic(tr, tname, vb, mirror):
-    """PMC bytes per launch of the batch's forward projector instantiation
-    (k_fwdg<T, VB, MIRROR, VBR>; mirror mode projects virtual width 2 x VBR)."""
+    """PMC bytes per launch of the batch's forward projector (fwd_kernel_name)."""
     if not tr:
         return None
-    want = f"admm::k_fwdg<{tname}, {min(2 * vb, 32 // (8 if tname == 'double' else 4)) if mirror else vb}, " \
-           f"{'true' if mirror else 'false'}, {vb}>"
-    return tr["kernels"].get(want, {}).get("hbm_bytes_per_launch")
+    return tr["kernels"].get(fwd_kernel_name(tr, tname, vb, mirror), {}).get("hbm_bytes_per_launch")
 
 
 KERNEL_SOURCES = ("distributed-inverse-problem-admm_amd/csrc/kernels.hpp",
@@ -609,8 +617,9 @@ def projector_rooflines(r, workload, fwd_reps):
     # forward taps: each node image read once, its sinogram written once (compulsory); the
     # design adds the transposed image copy (case-A angles) and the 8 segment partials
     fwd_comp = V * n * sb + V * m * sb
-    fwd = _roof((f"k_fwdg<{tname},{vbv},true,{vb}> (mirror mode: virtual {vbv}-lane images over half the "
-                 f"angles; " if mirror else f"k_fwdg<{tname},{vb}> (")
+    fname = fwd_kernel_name(tr, tname, vb, mirror).replace("admm::", "").replace(" ", "")
+    fwd = _roof((f"{fname} (mirror mode: virtual {vbv}-lane images over half the angles"
+                 f"{'; two virtual chunks per block' if fname.endswith(',2>') else ''}; " if mirror else f"{fname} (")
                 + f"Joseph forward projector taps, angle-grouped, 8 row-segment partial sums per ray; {chunks})",
                 fwd_kernel_traffic(tr, tname, vb, mirror), tr_file, fwd_ms, fwd_comp,
                 sb * a_node * n_img * 2 * n_img * V,  # m rays x N rows x 2 taps x V samples

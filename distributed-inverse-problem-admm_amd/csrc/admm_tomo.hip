@@ -121,6 +121,7 @@ struct admm_ctx {
   bool mirror_half = false;  // the half geometry of a mirror-mode context (XCD mapping below)
   Buf fg_order;                       // int4 block table of the grouped forward projector
   int fg_nblk = 0, fg_order_nch = 0;
+  int fg_cpb = 1;  // (mirror half geometry) virtual chunks per forward block of the bound table
   hipStream_t cap = nullptr;  // private capture stream
 
   // explicit-matrix context (admm_ctx_create_matrix): A and A^T as device CSR, values in
@@ -276,10 +277,10 @@ int build_fwd_order(admm_ctx* C, int pl, int nch, int cus) {
 // MIRROR / VBR: the instantiation launch_fwdg_taps launches (mirror mode: k_fwdg<T, VBV, true,
 // VBR>, whose piece state and second window buffer set its own registers and LDS), so the
 // occupancy query prices the kernel that actually runs.
-template <typename T, int VB, bool MIRROR = false, int VBR = VB>
-int pick_fwd_plan(admm_ctx* C, int nch, int* pl_out, int* cus_out) {
+template <typename T, int VB, bool MIRROR = false, int VBR = VB, int CPB = 1>
+int pick_fwd_plan(admm_ctx* C, int nch, int* pl_out, int* cus_out, long* slots_out = nullptr) {
   int per_cu = 0, cus = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fwdg<T, VB, MIRROR, VBR>, kFgThreads, 0));
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fwdg<T, VB, MIRROR, VBR, CPB>, kFgThreads, 0));
   HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, C->device));
   if (per_cu < 1) return fail(ADMM_E_HIP, "grouped forward projector cannot be resident");
   const long slots = (long)per_cu * std::max(1, cus);
@@ -294,13 +295,41 @@ int pick_fwd_plan(admm_ctx* C, int nch, int* pl_out, int* cus_out) {
   if (f && f[0] >= '0' && f[0] < '0' + admm_ctx::kPlans && C->plan_n[f[0] - '0'] > 0) pl = f[0] - '0';
   *pl_out = pl;
   *cus_out = cus;
+  if (slots_out) *slots_out = slots;
   return ADMM_OK;
+}
+
+// Two virtual chunks per forward block (k_fwdg CPB = 2: mirror mode, float32, one lane block per
+// real chunk) where the halved block table still fills every resident slot -- C3 and larger on
+// one GPU; the 8-node share of the scaling runs keeps one (its halved table would leave slots
+// empty).  ADMM_FWD_CPB=1 / 2 forces one / two (A/B and the bitwise tests; 2 needs an even
+// chunk count).
+template <typename T, int VB, bool MIRROR, int VBR>
+constexpr bool fwd_cpb2_ok() {
+  return MIRROR && std::is_same<T, float>::value && VB / 2 == VBR && VB == 8;
 }
 
 template <typename T, int VB, bool MIRROR = false, int VBR = VB>
 int choose_fwd_plan(admm_ctx* C, int V) {
   if (C->plan_n[0] == 0) return ADMM_OK;
   const int nch = (V + VB - 1) / VB;
+  C->fg_cpb = 1;
+  if constexpr (fwd_cpb2_ok<T, VB, MIRROR, VBR>()) {
+    const char* f = getenv("ADMM_FWD_CPB");
+    const int force = (f && f[0] >= '1' && f[0] <= '2') ? f[0] - '0' : 0;
+    if (nch % 2 == 0 && force != 1) {
+      int pl2 = 0, cus2 = 0;
+      long slots2 = 0;
+      RET((pick_fwd_plan<T, VB, MIRROR, VBR, 2>(C, nch / 2, &pl2, &cus2, &slots2)));
+      if (force == 2 || (long)C->plan_blocks[pl2] * (nch / 2) >= slots2) {
+        select_fwd_plan(C, pl2);
+        RET(build_fwd_order(C, pl2, nch / 2, cus2));
+        C->fg_order_nch = nch;
+        C->fg_cpb = 2;
+        return ADMM_OK;
+      }
+    }
+  }
   int pl = 0, cus = 0;
   RET((pick_fwd_plan<T, VB, MIRROR, VBR>(C, nch, &pl, &cus)));
   select_fwd_plan(C, pl);
@@ -427,6 +456,15 @@ int launch_fwdg_taps(admm_ctx* C, const T* img, const T* imgT, int V, hipStream_
     const int nchv = ((V + VB - 1) / VB) * (VB / MH);
     const admm_ctx* H = C->half;
     if (nchv != H->fg_order_nch) return fail(ADMM_E_STATE, "mirror block table built for another batch size");
+    if constexpr (fwd_cpb2_ok<T, VBV, true, VB>()) {
+      if (H->fg_cpb == 2) {  // two virtual chunks per block (the table holds chunk pairs)
+        hipLaunchKernelGGL((k_fwdg<T, VBV, true, VB, 2>), dim3(H->fg_nblk), dim3(kFgThreads), 0, s, img, imgT,
+                           (T*)C->fpart.p, H->fang, H->groups, H->rng, (const int4*)H->fg_order.p, C->g.N,
+                           C->g.n_det, H->g.n_angles, nchv * VBV);
+        CHECK_LAUNCH();
+        return ADMM_OK;
+      }
+    }
     hipLaunchKernelGGL((k_fwdg<T, VBV, true, VB>), dim3(H->fg_nblk), dim3(kFgThreads), 0, s, img, imgT,
                        (T*)C->fpart.p, H->fang, H->groups, H->rng, (const int4*)H->fg_order.p, C->g.N, C->g.n_det,
                        H->g.n_angles, nchv * VBV);

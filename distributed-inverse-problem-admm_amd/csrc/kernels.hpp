@@ -688,6 +688,9 @@ constexpr T kFgWScale = T(1);
 template <>
 constexpr float kFgWScale<float> = 2.3283064365386963e-10f;
 
+#ifndef ADMM_FG_WPE2
+#define ADMM_FG_WPE2 8  // the same for two chunks per block (CPB = 2)
+#endif
 #ifndef ADMM_FG_WPE
 #define ADMM_FG_WPE 8  // waves per SIMD the register budget must allow: <= 64 VGPRs, 2 blocks/CU
                        // (float64 samples otherwise take 67 and fall to one block per CU)
@@ -704,8 +707,13 @@ constexpr float kFgWScale<float> = 2.3283064365386963e-10f;
 // once per 8 lanes as in an 8-node batch -- and an 8-node batch runs two virtual chunks of
 // half the angles (the same taps).  Virtual chunk c' = real chunk c' / S, lane block c' % S of
 // VB/2 real lanes (S = 2 VBR / VB).
-template <typename T, int VB, bool MIRROR = false, int VBR = VB>
-__global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM_FG_WPE))) void k_fwdg(const T* __restrict__ img, const T* __restrict__ imgT,
+// CPB (round 6, mirror mode, float32): virtual chunks per block -- 2: one block projects the same
+// rays of chunks 2p and 2p + 1 (ob.z carries the pair p), a tap row's position, weights and LDS
+// slots formed once for both chunks' staged windows; the host uses it where the halved block
+// table still fills every slot (fwd_cpb).  Per chunk the arithmetic is CPB = 1's, in the same
+// order: bitwise the same partials.
+template <typename T, int VB, bool MIRROR = false, int VBR = VB, int CPB = 1>
+__global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(CPB == 1 ? ADMM_FG_WPE : ADMM_FG_WPE2))) void k_fwdg(const T* __restrict__ img, const T* __restrict__ imgT,
                                                  T* __restrict__ part, const FwdAngle* __restrict__ ang,
                                                  const FgGroup* __restrict__ groups, const FgRange* __restrict__ rng,
                                                  const int4* __restrict__ order, int N, int n_det, int n_ang, int V) {
@@ -723,7 +731,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   const int4 ob = order[blockIdx.x];
   const FgRange* rg = rng + ob.x;
   const FgGroup* gr = groups + ob.y;
-  const int seg = ob.z % kFgSeg, chunk = ob.z / kFgSeg;
+  const int seg = ob.z % kFgSeg, chunk = (ob.z / kFgSeg) * CPB;  // (CPB: the pair's first chunk)
   const int G = gr->G, t0 = gr->t0;
   const int npix = N * N;
   const int gq = min(g, G - 1);
@@ -750,13 +758,14 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   // rows per staged chunk (2 in the LDS-DMA kernel: the next chunk's DMA is issued a
   // 2-row chunk of taps ahead; 4-row chunks, or a 3/4-buffer ring with counted vmcnt waits
   // keeping 2-3 chunks in flight, measured slower)
+  static_assert(CPB == 1 || (kDma && MIRROR && MS == 1), "two chunks per block: LDS-DMA mirror kernel, one lane block per real chunk");
   constexpr int R = kDma ? ADMM_FG_DMA_ROWS : kFgRows;
   constexpr int PIECES = NPL * R * 2 * kFgPieces;  // 1-KiB LDS-DMA pieces per chunk
   // two NAMED chunk buffers (not one [2][...] array): the LDS-DMA into one and the tap reads of
   // the other then have distinct underlying objects, so the compiler's LDS-DMA alias tracking
   // does not put a vmcnt(0) -- a wait for the next chunk's DMA -- in front of the taps
-  __shared__ Pack<T, PV> win[NPL][R][kFgRow];
-  __shared__ Pack<T, PV> win1[kDma ? NPL : 1][kDma ? R : 1][kDma ? kFgRow : 1];
+  __shared__ Pack<T, PV> win[CPB][NPL][R][kFgRow];
+  __shared__ Pack<T, PV> win1[kDma ? CPB : 1][kDma ? NPL : 1][kDma ? R : 1][kDma ? kFgRow : 1];
   // every row window of the segment (N <= 4096): origin and the width actually touched
   __shared__ __align__(16) int wlo_s[(4096 + kFgSeg - 1) / kFgSeg + 4];  // +4: int4 reads of the last chunk
   __shared__ int wnum_s[(4096 + kFgSeg - 1) / kFgSeg + 4];
@@ -798,9 +807,11 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   // (|error| <= rows * 2^-33 pixel, below the float32 weights' own rounding)
   long long lfix = llrint(fma((double)m_lo, a.dl, l0) * 4294967296.0);
   const long long dlfix = llrint(a.dl * 4294967296.0);
-  T acc[VB];
+  T acc[CPB][VB];
 #pragma unroll
-  for (int u = 0; u < VB; ++u) acc[u] = T(0);
+  for (int c = 0; c < CPB; ++c)
+#pragma unroll
+    for (int u = 0; u < VB; ++u) acc[c][u] = T(0);
   int wl_cur[R];  // the current chunk's window origins (scalars)
   // the chunk's window origins, read once into scalar registers (a per-row LDS read
   // would put a dependent LDS round trip in front of every row's tap reads)
@@ -821,7 +832,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
     }
   };
   // the taps of one staged chunk: every row's two taps per ray from LDS
-  auto taps = [&](const Pack<T, PV> (&wb)[NPL][R][kFgRow], int m0, int rows, const int (&wl)[R]) {
+  auto taps = [&](const Pack<T, PV> (&wb)[CPB][NPL][R][kFgRow], int m0, int rows, const int (&wl)[R]) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {  // unrolled: the chunk's LDS reads can all be in flight
       if (r >= rows) break;
@@ -843,22 +854,24 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
       const int se = (idx + 1) >> 1, so = kFgOdd + (idx >> 1);
       const T we = odd ? w1 : w0, wo = odd ? w0 : w1;
 #pragma unroll
-      for (int q = 0; q < NPL; ++q) {
-        const Pack<T, PV> s0 = wb[q][r][se];
-        const Pack<T, PV> s1 = wb[q][r][so];
+      for (int c = 0; c < CPB; ++c)
 #pragma unroll
-        for (int e = 0; e < PV; ++e) {
-          acc[q * PV + e] = fma(we, s0.v[e], acc[q * PV + e]);
-          acc[q * PV + e] = fma(wo, s1.v[e], acc[q * PV + e]);
+        for (int q = 0; q < NPL; ++q) {
+          const Pack<T, PV> s0 = wb[c][q][r][se];
+          const Pack<T, PV> s1 = wb[c][q][r][so];
+#pragma unroll
+          for (int e = 0; e < PV; ++e) {
+            acc[c][q * PV + e] = fma(we, s0.v[e], acc[c][q * PV + e]);
+            acc[c][q * PV + e] = fma(wo, s1.v[e], acc[c][q * PV + e]);
+          }
         }
-      }
     }
   };
   // Software-pipelined full chunk: every row's tap slots and weights first,
   // then row r+1's LDS reads issued before row r's FMAs, so one row's reads are always in
   // flight behind the other's arithmetic (the LDS-DMA staging freed the registers: the
   // register-staged kernel had no room for the second row's 16).  Same FMAs, same order.
-  auto taps4 = [&](const Pack<T, PV> (&wb)[NPL][R][kFgRow], int m0) {
+  auto taps4 = [&](const Pack<T, PV> (&wb)[CPB][NPL][R][kFgRow], int m0) {
     int se[R], so[R];  // (float: byte offsets of the even / odd slot; else slot indices)
     T we[R], wo[R];
 #pragma unroll
@@ -898,36 +911,39 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         wo[r] = odd ? w0 : w1;
       }
     }
-    // the even / odd tap samples of row r, plane q
-    auto slot = [&](int q, int r, bool even) -> Pack<T, PV> {
+    // the even / odd tap samples of row r, plane q, chunk c
+    auto slot = [&](int c, int q, int r, bool even) -> Pack<T, PV> {
       if constexpr (std::is_same<T, float>::value) {
-        const char* row = reinterpret_cast<const char*>(&wb[q][r][0]);
+        const char* row = reinterpret_cast<const char*>(&wb[c][q][r][0]);
         return *reinterpret_cast<const Pack<T, PV>*>(even ? row + se[r] : row + kFgOdd * (int)sizeof(Pack<T, PV>) + so[r]);
       } else {
-        return wb[q][r][even ? se[r] : so[r]];
+        return wb[c][q][r][even ? se[r] : so[r]];
       }
     };
+    // (row, chunk) steps in order; step s + 1's LDS reads issued before step s's FMAs
     Pack<T, PV> cur[2 * NPL], nxt[2 * NPL];
 #pragma unroll
     for (int q = 0; q < NPL; ++q) {
-      cur[2 * q] = slot(q, 0, true);
-      cur[2 * q + 1] = slot(q, 0, false);
+      cur[2 * q] = slot(0, q, 0, true);
+      cur[2 * q + 1] = slot(0, q, 0, false);
     }
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (r + 1 < R) {
+    for (int st = 0; st < R * CPB; ++st) {
+      const int r = st / CPB, c = st % CPB;
+      if (st + 1 < R * CPB) {
+        const int r1 = (st + 1) / CPB, c1 = (st + 1) % CPB;
 #pragma unroll
         for (int q = 0; q < NPL; ++q) {
-          nxt[2 * q] = slot(q, r + 1, true);
-          nxt[2 * q + 1] = slot(q, r + 1, false);
+          nxt[2 * q] = slot(c1, q, r1, true);
+          nxt[2 * q + 1] = slot(c1, q, r1, false);
         }
       }
 #pragma unroll
       for (int q = 0; q < NPL; ++q)
 #pragma unroll
         for (int e = 0; e < PV; ++e) {
-          acc[q * PV + e] = fma(we[r], cur[2 * q].v[e], acc[q * PV + e]);
-          acc[q * PV + e] = fma(wo[r], cur[2 * q + 1].v[e], acc[q * PV + e]);
+          acc[c][q * PV + e] = fma(we[r], cur[2 * q].v[e], acc[c][q * PV + e]);
+          acc[c][q * PV + e] = fma(wo[r], cur[2 * q + 1].v[e], acc[c][q * PV + e]);
         }
 #pragma unroll
       for (int q = 0; q < 2 * NPL; ++q) cur[q] = nxt[q];
@@ -1007,12 +1023,20 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         // VALU than the L2 fetch it saved)
         const unsigned voff = MIRROR ? (unsigned)((col * VBR + mq * MH) * (int)sizeof(T))
                                      : (unsigned)((col * VB + P.ppl * PV) * (int)sizeof(T));
-        if (b == 0)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              rs, (__attribute__((address_space(3))) void*)&win[P.ppl][P.pr][P.pslot], 16, voff, 0, 0, 0);
-        else
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              rs, (__attribute__((address_space(3))) void*)&win1[P.ppl][P.pr][P.pslot], 16, voff, 0, 0, 0);
+#pragma unroll
+        for (int c = 0; c < CPB; ++c) {
+          // (chunk c of the pair: the next real chunk's image, npix x VBR samples further)
+          const __amdgpu_buffer_rsrc_t rsc =
+              c == 0 ? rs
+                     : make_rsrc((const void*)(uintptr_t)((((uint64_t)hi << 32) | lo) + (uint64_t)c * npix * VBR * sizeof(T)),
+                                 rowbytes);
+          if (b == 0)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rsc, (__attribute__((address_space(3))) void*)&win[c][P.ppl][P.pr][P.pslot], 16, voff, 0, 0, 0);
+          else
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rsc, (__attribute__((address_space(3))) void*)&win1[c][P.ppl][P.pr][P.pslot], 16, voff, 0, 0, 0);
+        }
       }
     };
     dma(m_lo, 0, std::false_type{});
@@ -1108,7 +1132,7 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
         if (q < R * kFgWin * NPL) {
           const int pl = q % NPL, rw = q / NPL;
           const int r = rw / kFgWin, w = rw - r * kFgWin;
-          win[pl][r][(w & 1) ? kFgOdd + (w >> 1) : (w >> 1)] = stage[e];
+          win[0][pl][r][(w & 1) ? kFgOdd + (w >> 1) : (w >> 1)] = stage[e];
         }
       }
     };
@@ -1128,7 +1152,10 @@ __global__ __launch_bounds__(kFgThreads) __attribute__((amdgpu_waves_per_eu(ADMM
   }
   if (g < G && rl < nkq) {
     const size_t m_rays = (size_t)n_ang * n_det;
-    gstore<T, VB>(part + (((size_t)seg * ((V + VB - 1) / VB) + chunk) * m_rays + (size_t)t * n_det + k) * VB, acc);
+#pragma unroll
+    for (int c = 0; c < CPB; ++c)
+      gstore<T, VB>(part + (((size_t)seg * ((V + VB - 1) / VB) + chunk + c) * m_rays + (size_t)t * n_det + k) * VB,
+                    acc[c]);
   }
 }
 

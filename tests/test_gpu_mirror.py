@@ -117,18 +117,20 @@ def test_default_mode_by_sample_type(cuda, monkeypatch):
 
 @pytest.mark.parametrize("dtype,V,N", [("float32", 5, 64), ("float32", 16, 128), ("float32", 4, 47),
                                        ("float64", 2, 48)])
-def test_back_windows_by_lds_dma_bitwise(cuda, monkeypatch, dtype, V, N):
+def test_projector_block_shapes_bitwise(cuda, monkeypatch, dtype, V, N):
     """The mirror back projector's H mode stages its sinogram windows by LDS-DMA into two
     chunk buffers (kernels.hpp k_back_mirror, DMA), and where the grid fills the chip runs two
     lane blocks per block (k_back_mirror_2); ADMM_BK_STAGING at context creation selects
     "dma1" (one lane block per block), "reg" (register-staged windows) or "dma2" (two lane
     blocks wherever they pair up).  The same bins land in LDS and every lane block's taps read
     them in the same order: whole trajectories bitwise equal (5 nodes = a full and a one-node
-    lane block; 16 nodes = four lane blocks; odd N; float64 keeps one lane block)."""
+    lane block; 16 nodes = four lane blocks; odd N; float64 keeps one lane block).  The forward
+    projector likewise with one or two virtual chunks per block (ADMM_FWD_CPB=1 / 2, k_fwdg CPB)."""
     monkeypatch.setenv("ADMM_FWD_MIRROR", "1")
     runs = []
-    for staging in ("dma1", "reg", "dma2"):
+    for staging, fcpb in (("dma1", "1"), ("reg", "1"), ("dma2", "2")):
         monkeypatch.setenv("ADMM_BK_STAGING", staging)
+        monkeypatch.setenv("ADMM_FWD_CPB", fcpb)
         _, _, _, _, _, x, h = _run(N, V, 24, dtype)
         runs.append((x, {k: np.asarray(h[k]) for k in ("primal", "dual", "obj_total", "mse_sino_total",
                                                        "g_norm_history")}))
