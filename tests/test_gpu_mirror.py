@@ -116,7 +116,7 @@ def test_default_mode_by_sample_type(cuda, monkeypatch):
 
 
 @pytest.mark.parametrize("dtype,V,N", [("float32", 5, 64), ("float32", 16, 128), ("float32", 4, 47),
-                                       ("float64", 2, 48)])
+                                       ("float32", 8, 47), ("float64", 2, 48)])
 def test_projector_block_shapes_bitwise(cuda, monkeypatch, dtype, V, N):
     """The mirror back projector's H mode stages its sinogram windows by LDS-DMA into two
     chunk buffers (kernels.hpp k_back_mirror, DMA), and where the grid fills the chip runs two
